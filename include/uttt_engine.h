@@ -1,0 +1,182 @@
+/*
+ * uttt_engine.h — C ABI of the MI355X-native Ultimate Tic-Tac-Toe self-play engine.
+ *
+ * This is the drop-in boundary for the reference's native hot path
+ * (cpp/uttt_game.h, cpp/uttt_mcts.h behind the pybind11 module `uttt_cpp`,
+ * cpp/python_bindings.cpp:49-107). Plain C types only: pointers, sizes,
+ * status codes. Every function returns UTTT_OK (0) or a negative UTTT_ERR_*;
+ * uttt_last_error() gives the message of the calling thread's last failure.
+ *
+ * Two layers:
+ *   1. Rules on one host-side state value (what `uttt_cpp.State` binds).
+ *   2. The engine: thousands of PUCT trees in SoA arrays in HBM, advanced in
+ *      lock-step rounds by HIP kernels (gfx950). A round = every unfinished
+ *      tree descends to its next unevaluated leaf (absorbing terminal
+ *      simulations), the leaves are handed to an evaluator as one NCHW batch,
+ *      and the results are expanded + backed up. Self-play adds the per-move
+ *      policy target, numpy-exact move sampling and game records on device.
+ *
+ * Semantics are those of cpp/uttt_mcts.cpp:84-196 bit for bit (see DESIGN.md,
+ * "Exact semantics"); the only structural change is that the k identical
+ * copies of a flushed leaf (uttt_mcts.cpp:121-135 queues the same leaf k times
+ * because there is no virtual loss) are evaluated once and replayed k times.
+ */
+#ifndef UTTT_ENGINE_H
+#define UTTT_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UTTT_OK 0
+#define UTTT_ERR_ARG (-1)      /* invalid argument                                  */
+#define UTTT_ERR_HIP (-2)      /* HIP runtime error                                 */
+#define UTTT_ERR_CAPACITY (-3) /* node pool / path / record arena exhausted         */
+#define UTTT_ERR_ORDER (-4)    /* call out of sequence (e.g. apply before select)   */
+#define UTTT_ERR_NODEVICE (-5) /* no gfx950 device / device ordinal out of range    */
+
+#define UTTT_ACTIONS 81
+#define UTTT_INPUT_SIZE 243 /* (3, 9, 9) NCHW f32 per position */
+
+/* Packed, side-to-move-relative position (32 bytes; same bits on host and device).
+ * own[w]/opp[w]: small boards 3w..3w+2, board b's 9 cells at bits 9*(b%3)..+8,
+ *   so bit (a % 27) of word (a / 27) is action a = board*9 + cell.
+ * mains: bits 0..8 main_board_pieces, bits 16..24 main_board_enemy_pieces.
+ * active: -1 (any board) or 0..8.
+ * Replaces UTTT::State's int arrays (cpp/uttt_game.h:49-54). */
+typedef struct uttt_state {
+    uint32_t own[3];
+    uint32_t opp[3];
+    uint32_t mains;
+    int32_t active;
+} uttt_state_t;
+
+const char *uttt_last_error(void);
+const char *uttt_version(void);
+
+/* ---------------------------------------------------------------- rules --- */
+/* State() — cpp/uttt_game.cpp:9-21 */
+void uttt_state_initial(uttt_state_t *out);
+/* State(pieces, enemy_pieces, main, main_enemy, active) — cpp/uttt_game.cpp:24-32.
+ * Arrays are [board][cell] row-major. Values must be 0/1 and active in -1..8
+ * (the reference does not validate; out-of-range input is UB there). */
+int uttt_state_from_arrays(const int32_t pieces[81], const int32_t enemy_pieces[81],
+                           const int32_t main_board_pieces[9], const int32_t main_board_enemy_pieces[9],
+                           int32_t active_board, uttt_state_t *out);
+/* get_pieces/... — cpp/uttt_game.h:42-46 */
+void uttt_state_to_arrays(const uttt_state_t *s, int32_t pieces[81], int32_t enemy_pieces[81],
+                          int32_t main_board_pieces[9], int32_t main_board_enemy_pieces[9],
+                          int32_t *active_board);
+/* State::next — cpp/uttt_game.cpp:97-145 (any action 0..80, unvalidated as in the reference) */
+int uttt_state_next(const uttt_state_t *s, int32_t action, uttt_state_t *out);
+/* State::legal_actions — cpp/uttt_game.cpp:148-191; returns the count, ascending actions in out */
+int uttt_state_legal_actions(const uttt_state_t *s, int32_t out[81]);
+/* is_lose / is_draw / is_done / is_first_player — cpp/uttt_game.cpp:77-94 (return 0/1) */
+int uttt_state_is_lose(const uttt_state_t *s);
+int uttt_state_is_draw(const uttt_state_t *s);
+int uttt_state_is_done(const uttt_state_t *s);
+int uttt_state_is_first_player(const uttt_state_t *s);
+/* to_input_tensor — cpp/uttt_game.cpp:244-280 (HWC (9,9,3) flat) */
+void uttt_state_input_hwc(const uttt_state_t *s, float out[243]);
+/* to_string — cpp/uttt_game.cpp:194-241; returns length, or -(needed) if cap too small */
+int uttt_state_to_string(const uttt_state_t *s, char *buf, int32_t cap);
+/* boltzman — cpp/uttt_mcts.cpp:199-216 */
+int uttt_boltzman(const float *xs, int32_t n, float temperature, float *out);
+
+/* --------------------------------------------------------------- engine --- */
+typedef struct uttt_engine uttt_engine_t;
+
+/* device: HIP ordinal (-1 = the calling thread's current device). max_trees: concurrent trees / game slots. max_sims: the
+ * largest evaluate_count this engine will run (sizes the node pool to the
+ * exact worst case 82 + 81*max_sims nodes per tree, so it cannot overflow). */
+int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out);
+int uttt_engine_destroy(uttt_engine_t *eng);
+/* Launch everything on `stream` (a hipStream_t, e.g. torch's current stream);
+ * NULL restores the engine's own stream. */
+int uttt_engine_set_stream(uttt_engine_t *eng, void *stream);
+/* Device bytes held by the engine. */
+int64_t uttt_engine_device_bytes(const uttt_engine_t *eng);
+
+/* Start a search of n_trees independent trees (pv_mcts_scores,
+ * uttt_mcts.cpp:92-103: root expanded with uniform priors 1/|legal|).
+ * roots: host array of n_trees states. */
+int uttt_search_begin(uttt_engine_t *eng, const uttt_state_t *roots, int32_t n_trees, int32_t evaluate_count,
+                      int32_t batch_size);
+
+/* One round of descents (uttt_mcts.cpp:109-127). Writes the pending leaves'
+ * network inputs, NCHW (n,3,9,9) f32, to device memory nn_input (room for
+ * max_trees*243 floats; may be NULL) in deterministic tree order, and stores
+ * the number of pending leaves in *n_pending (0 = search finished). Blocks on
+ * the stream to read the count. */
+int uttt_search_select(uttt_engine_t *eng, float *nn_input, int32_t *n_pending);
+
+/* Host copies of the pending leaves (slot order) and their multiplicity k
+ * (the number of identical copies the reference would have queued). */
+int uttt_search_pending(uttt_engine_t *eng, uttt_state_t *states, int32_t *copies);
+
+/* Evaluator results for the pending leaves (uttt_mcts.cpp:138-167: legal-mask,
+ * sequential f32 renormalisation, expand k times, back up k times).
+ * Row r of policy (>= 81 f32, stride policy_ld) / value (stride value_ld)
+ * belongs to pending slot r. per_copy != 0: the rows are per queued copy
+ * (slot 0's k copies first, then slot 1's ...), as the reference's model()
+ * batch is. on_device: pointers are device (else host, copied on the stream). */
+int uttt_search_apply(uttt_engine_t *eng, const float *policy, int64_t policy_ld, const float *value,
+                      int64_t value_ld, int32_t per_copy, int32_t on_device);
+
+/* Deterministic hash evaluator on device (test / micro-benchmark evaluator;
+ * DESIGN.md "Hash evaluator"): n rows of nn_input -> policy (n,81), value (n). */
+int uttt_eval_hash(uttt_engine_t *eng, const float *nn_input, int32_t n, float *policy, float *value);
+
+/* Root results after the search: visit counts of the root's children (legal
+ * order, row stride 81) and |legal| per tree. */
+int uttt_search_root_visits(uttt_engine_t *eng, int32_t *visits, int32_t *n_legal);
+/* Scores as pv_mcts_scores returns them (uttt_mcts.cpp:177-195): one-hot first
+ * max for temperature 0, else boltzman; row stride 81. */
+int uttt_search_scores(uttt_engine_t *eng, float temperature, float *scores, int32_t *n_legal);
+
+/* -------------------------------------------------------------- self-play --- */
+/* Self-play of games [game_begin, game_end) (self_play_cpp.py:34-130), each
+ * game g with its own numpy-legacy MT19937 seeded seed_base + g (=
+ * np.random.seed(seed_base + g) before self_play_cpp.play). Slots are refilled
+ * with the next game id as games end. arena_plies bounds the finished-game
+ * record arena (plies). */
+int uttt_selfplay_begin(uttt_engine_t *eng, int64_t game_begin, int64_t game_end, uint32_t seed_base,
+                        float temperature, int32_t evaluate_count, int32_t batch_size, int64_t arena_plies);
+/* Start one move for every live game: its search tree is rebuilt from the
+ * current position (no tree reuse, uttt_mcts.cpp:92). *n_live = live slots
+ * (0 = every game finished). Then run select/eval/apply rounds. */
+int uttt_selfplay_move_begin(uttt_engine_t *eng, int32_t *n_live);
+/* Finish the move (self_play_cpp.py:63-92): scores -> f64 policy target
+ * (np.sum renormalisation) -> np.random.choice -> record -> next state;
+ * ended games get their values (self_play_cpp.py:95-99) and are written to
+ * the arena; free slots take the next game. *n_finished = games in the arena. */
+int uttt_selfplay_move_end(uttt_engine_t *eng, int64_t *n_finished);
+/* numpy-legacy MT19937 state of a slot's current game (624 words + position),
+ * so a caller can run a game on numpy's global RandomState and continue it
+ * afterwards (self_play_cpp.play draws from np.random, self_play_cpp.py:86). */
+int uttt_selfplay_get_rng(uttt_engine_t *eng, int32_t slot, uint32_t key[624], int32_t *pos);
+int uttt_selfplay_set_rng(uttt_engine_t *eng, int32_t slot, const uint32_t key[624], int32_t pos);
+/* Finished games: n_games entries of (game id, first ply in arena, plies),
+ * sorted by game id; then the arena rows [0, n_plies): state, policy target
+ * (81 f64), action, value. Any output pointer may be NULL. */
+int uttt_selfplay_games(uttt_engine_t *eng, int64_t *game_ids, int64_t *offsets, int32_t *lengths,
+                        int64_t max_games, int64_t *n_games);
+int uttt_selfplay_plies(uttt_engine_t *eng, uttt_state_t *states, double *policies, int8_t *actions,
+                        int8_t *values, float *inputs_hwc, int64_t max_plies, int64_t *n_plies);
+
+/* ------------------------------------------------------------ telemetry --- */
+/* Per-kernel timing with HIP events on the engine's stream (off by default). */
+int uttt_engine_set_timing(uttt_engine_t *eng, int32_t enabled);
+/* kernel: 0 select, 1 apply, 2 encode, 3 scan, 4 move_end, 5 hash_eval.
+ * Outputs total ms, launches and algorithmic bytes. */
+int uttt_engine_kernel_stats(uttt_engine_t *eng, int32_t kernel, double *total_ms, int64_t *launches,
+                             int64_t *algo_bytes);
+int uttt_engine_reset_stats(uttt_engine_t *eng);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UTTT_ENGINE_H */

@@ -1,0 +1,211 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container (it needs /root/reference and oracle/_ref/,
+built by ``make -C oracle``). The committed .npz files are data: inputs and the
+reference's outputs on them. Nothing of the reference's source travels.
+
+Sources of truth used here:
+  * oracle/_ref/libuttt_ref.so — cpp/uttt_game.cpp + cpp/uttt_mcts.cpp compiled
+    from the reference checkout (rules, pv_mcts_scores with the hash evaluator);
+  * oracle/_ref/uttt_cpp*.so + the reference's self_play_cpp.py / pv_mcts_cpp.py
+    imported from /root/reference (self-play with numpy's global RNG seeded
+    per game), driven by oracle.hashnp.HashModel;
+  * the reference's dual_network.py (DualNetwork under torch.manual_seed(0),
+    CPU fp32) for the network I/O fixture.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import json
+import os
+import random
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, REPO)
+
+from oracle import ref  # noqa: E402
+
+SEARCH_CONFIGS = [(50, 8), (50, 1), (50, 1024), (400, 8), (10, 2), (30, 3), (1, 1), (7, 100), (64, 64)]
+TEMPERATURES = [1.0, 0.0, 0.5]
+
+
+def initial():
+    return (np.zeros((9, 9), np.int32), np.zeros((9, 9), np.int32), np.zeros(9, np.int32),
+            np.zeros(9, np.int32), -1)
+
+
+def pack(st):
+    p, e, m, me, a = st
+    return (np.asarray(p, np.uint8).reshape(81), np.asarray(e, np.uint8).reshape(81),
+            np.asarray(m, np.uint8), np.asarray(me, np.uint8), np.int8(a))
+
+
+def gen_rules(n_games=120, seed=7):
+    rng = random.Random(seed)
+    cols = {k: [] for k in ("pieces", "enemy", "main_p", "main_e", "active", "legal", "n_legal",
+                            "flags", "tensor", "action", "game")}
+    odd = {k: [] for k in ("pieces", "enemy", "main_p", "main_e", "active", "action",
+                           "n_pieces", "n_enemy", "n_main_p", "n_main_e", "n_active")}
+    strings = []
+    q7 = 0
+    for g in range(n_games):
+        st = initial()
+        while True:
+            legal = ref.legal_actions(st)
+            fl = ref.flags(st)
+            p, e, m, me, a = pack(st)
+            mask = np.zeros(81, np.uint8)
+            mask[legal] = 1
+            t = ref.tensor(st)
+            act = rng.choice(legal) if legal else -1
+            for k, v in (("pieces", p), ("enemy", e), ("main_p", m), ("main_e", me), ("active", a),
+                         ("legal", mask), ("n_legal", len(legal)), ("flags", fl),
+                         ("tensor", t.astype(np.uint8)), ("action", act), ("game", g)):
+                cols[k].append(v)
+            if (rng.random() < 0.02 or not legal) and len(strings) < 48:
+                strings.append({"state": [p.tolist(), e.tolist(), m.tolist(), me.tolist(), int(a)],
+                                "text": ref.to_string(st)})
+            # next() on arbitrary in-range actions (occupied cells, closed boards): pin the
+            # reference's unvalidated transition (uttt_game.cpp:97-145)
+            if rng.random() < 0.15:
+                ax = rng.randrange(81)
+                nx = pack(ref.next_state(st, ax))
+                for k, v in (("pieces", p), ("enemy", e), ("main_p", m), ("main_e", me), ("active", a),
+                             ("action", ax), ("n_pieces", nx[0]), ("n_enemy", nx[1]), ("n_main_p", nx[2]),
+                             ("n_main_e", nx[3]), ("n_active", nx[4])):
+                    odd[k].append(v)
+            if not legal:
+                break
+            nst = ref.next_state(st, act)
+            b = act // 9
+            if nst[2][b] == 1 and nst[3][b] == 1:
+                q7 += 1
+            st = nst
+    out = {k: np.asarray(v) for k, v in cols.items()}
+    out.update({"odd_" + k: np.asarray(v) for k, v in odd.items()})
+    return out, strings, q7
+
+
+def sample_positions(rules, n=40, seed=11):
+    rng = np.random.RandomState(seed)
+    live = np.nonzero(rules["n_legal"] > 0)[0]
+    idx = rng.choice(live, size=n, replace=False)
+    pos = []
+    for i in sorted(idx.tolist()):
+        pos.append((rules["pieces"][i].reshape(9, 9).astype(np.int32), rules["enemy"][i].reshape(9, 9).astype(np.int32),
+                    rules["main_p"][i].astype(np.int32), rules["main_e"][i].astype(np.int32), int(rules["active"][i])))
+    return pos
+
+
+def win_in_one():
+    """Side to move can win the game now (SURVEY App. A Q4 case)."""
+    p, e, m, me, _ = initial()
+    # side to move owns small boards 0 and 1; board 2 has own stones on cells 0,1
+    m[0] = m[1] = 1
+    for b in (0, 1):
+        p[b, 0] = p[b, 1] = p[b, 2] = 1
+    p[2, 0] = p[2, 1] = 1
+    e[3, 0] = e[3, 4] = e[4, 4] = e[5, 8] = e[6, 2] = e[7, 5] = e[8, 1] = 1
+    e[2, 4] = 1
+    return (p, e, m, me, 2)
+
+
+def gen_search(positions):
+    out = {"pos_" + k: [] for k in ("pieces", "enemy", "main_p", "main_e", "active")}
+    for st in positions:
+        p, e, m, me, a = pack(st)
+        for k, v in (("pieces", p), ("enemy", e), ("main_p", m), ("main_e", me), ("active", a)):
+            out["pos_" + k].append(v)
+    res = {"scores": [], "n": [], "pos": [], "sims": [], "batch": [], "temp": [], "flushes": [], "evals": [],
+           "uniq": []}
+    for pi, st in enumerate(positions):
+        for (S, B) in SEARCH_CONFIGS:
+            for tau in TEMPERATURES:
+                sc, stats = ref.search_hash(st, tau, S, B)
+                row = np.zeros(81, np.float32)
+                row[:sc.size] = sc
+                for k, v in (("scores", row), ("n", sc.size), ("pos", pi), ("sims", S), ("batch", B), ("temp", tau),
+                             ("flushes", stats[0]), ("evals", stats[1]), ("uniq", stats[2])):
+                    res[k].append(v)
+    out = {k: np.asarray(v) for k, v in out.items()}
+    out.update({k: np.asarray(v) for k, v in res.items()})
+    return out
+
+
+def gen_selfplay(n_games=12, base_seed=1234):
+    sys.path[:0] = [ref.REF_DIR, REF]
+    import self_play_cpp  # reference driver (imports the reference-built uttt_cpp)
+    from oracle.hashnp import make_hash_model
+    model = make_hash_model()
+    T, P, A, V, L, S = [], [], [], [], [], []
+    real_choice = np.random.choice
+
+    def recording_choice(*args, **kw):  # same RNG stream; just records the pick
+        r = real_choice(*args, **kw)
+        A.append(int(r))
+        return r
+
+    np.random.choice = recording_choice
+    try:
+        for g in range(n_games):
+            np.random.seed(base_seed + g)
+            h = self_play_cpp.play(model, True)
+            for rec in h:
+                T.append(np.asarray(rec[0], np.float32).reshape(243).astype(np.uint8))
+                P.append(np.asarray(rec[1], np.float64))
+                V.append(int(rec[2]))
+            L.append(len(h))
+            S.append(base_seed + g)
+    finally:
+        np.random.choice = real_choice
+    assert len(A) == len(T)
+    return {"tensors": np.asarray(T), "policies": np.asarray(P), "actions": np.asarray(A, np.int8),
+            "values": np.asarray(V, np.int8), "lengths": np.asarray(L, np.int32),
+            "seeds": np.asarray(S, np.int64)}
+
+
+def gen_network(n_states=24):
+    sys.path[:0] = [REF]
+    import torch
+    import dual_network  # reference network definition
+    torch.manual_seed(0)
+    net = dual_network.DualNetwork().eval()
+    rules = np.load(os.path.join(HERE, "rules.npz"))
+    idx = np.linspace(0, len(rules["n_legal"]) - 1, n_states).astype(int)
+    hwc = rules["tensor"][idx].astype(np.float32).reshape(-1, 9, 9, 3)
+    x = torch.from_numpy(np.ascontiguousarray(hwc.transpose(0, 3, 1, 2)))
+    with torch.no_grad():
+        p, v = net(x)
+    # a fingerprint of the seed-0 weights (sum per tensor, f64) pins the init order
+    fp = np.asarray([t.double().sum().item() for t in net.state_dict().values()], np.float64)
+    names = np.asarray(list(net.state_dict().keys()))
+    return {"x": x.numpy(), "policy": p.numpy(), "value": v.numpy(), "param_sums": fp, "param_names": names}
+
+
+def main():
+    assert ref.available(), "build oracle/_ref first: make -C oracle"
+    rules, strings, q7 = gen_rules()
+    np.savez_compressed(os.path.join(HERE, "rules.npz"), **rules)
+    with open(os.path.join(HERE, "to_string.json"), "w") as f:
+        json.dump(strings, f, indent=0)
+    print("rules:", len(rules["n_legal"]), "states; drawn small boards (Q7):", q7, "; odd next():",
+          len(rules["odd_action"]))
+    positions = sample_positions(rules) + [initial(), win_in_one()]
+    search = gen_search(positions)
+    np.savez_compressed(os.path.join(HERE, "search.npz"), **search)
+    print("search:", len(search["n"]), "cases; max unique leaves per flush:", int(search["uniq"].max()))
+    sp = gen_selfplay()
+    np.savez_compressed(os.path.join(HERE, "selfplay.npz"), **sp)
+    print("selfplay:", len(sp["lengths"]), "games,", int(sp["lengths"].sum()), "plies")
+    nn = gen_network()
+    np.savez_compressed(os.path.join(HERE, "network.npz"), **nn)
+    print("network:", nn["x"].shape[0], "states")
+
+
+if __name__ == "__main__":
+    main()

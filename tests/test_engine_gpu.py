@@ -1,0 +1,278 @@
+"""GPU parity tests: the HIP engine against the golden fixtures (the reference's
+own outputs) and against the CPU oracle, bit for bit, through the C ABI.
+
+Evaluators: the device hash evaluator (deterministic, exercises zero /
+subnormal / sparse priors) and the real DualNetwork, whose outputs are
+recorded and replayed into the oracle so search parity is checked
+independently of network numerics."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [(50, 8), (50, 1), (50, 1024), (400, 8), (10, 2), (30, 3), (1, 1), (7, 100), (64, 64)]
+
+
+def _pos_states(d):
+    from uttt_amd._lib import STATE_DTYPE
+    n = len(d["pos_active"])
+    out = np.zeros(n, STATE_DTYPE)
+    for i in range(n):
+        p = d["pos_pieces"][i].astype(np.uint32)
+        e = d["pos_enemy"][i].astype(np.uint32)
+        for a in range(81):
+            out["own"][i, a // 27] |= p[a] << (a % 27)
+            out["opp"][i, a // 27] |= e[a] << (a % 27)
+        mains = 0
+        for b in range(9):
+            mains |= int(d["pos_main_p"][i][b]) << b
+            mains |= int(d["pos_main_e"][i][b]) << (16 + b)
+        out["mains"][i] = mains
+        out["active"][i] = d["pos_active"][i]
+    return out
+
+
+def _oracle_state(core, st):
+    p = np.zeros(81, np.int32)
+    e = np.zeros(81, np.int32)
+    for a in range(81):
+        p[a] = (int(st["own"][a // 27]) >> (a % 27)) & 1
+        e[a] = (int(st["opp"][a // 27]) >> (a % 27)) & 1
+    mp = [(int(st["mains"]) >> b) & 1 for b in range(9)]
+    me = [(int(st["mains"]) >> (16 + b)) & 1 for b in range(9)]
+    return core.OrState.from_arrays(p.reshape(9, 9), e.reshape(9, 9), mp, me, int(st["active"]))
+
+
+def _random_positions(core, n, seed):
+    from uttt_amd import as_states  # noqa: F401
+    from uttt_amd._lib import STATE_DTYPE
+    rng = random.Random(seed)
+    out = []
+    while len(out) < n:
+        s = core.OrState.initial()
+        while not s.is_done() and len(out) < n:
+            if rng.random() < 0.3:
+                out.append(s)
+            s = s.next(rng.choice(s.legal_actions()))
+    arr = np.zeros(n, STATE_DTYPE)
+    for i, s in enumerate(out):
+        p, e, mp, me, a = s.arrays()
+        for x in range(81):
+            arr["own"][i, x // 27] |= int(p.reshape(81)[x]) << (x % 27)
+            arr["opp"][i, x // 27] |= int(e.reshape(81)[x]) << (x % 27)
+        arr["mains"][i] = sum(int(mp[b]) << b for b in range(9)) | sum(int(me[b]) << (16 + b) for b in range(9))
+        arr["active"][i] = a
+    return arr, out
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import uttt_amd
+    return uttt_amd
+
+
+def test_search_matches_golden(gpu, oracle_lib):
+    d = golden("search.npz")
+    roots = _pos_states(d)
+    bs = gpu.BatchedSearch(len(roots), 400)
+    ev = gpu.HashEvaluator(bs.engine)
+    checked = 0
+    for (S, B) in CONFIGS:
+        bs.run(roots, ev, S, B)
+        for tau in (1.0, 0.0, 0.5):
+            sc, L = bs.scores(tau)
+            rows = np.nonzero((d["sims"] == S) & (d["batch"] == B) & (d["temp"] == np.float32(tau)))[0]
+            assert len(rows) == len(roots)
+            for r in rows:
+                pi = int(d["pos"][r])
+                n = int(d["n"][r])
+                assert L[pi] == n
+                assert np.array_equal(sc[pi, :n].view(np.uint32), d["scores"][r][:n].view(np.uint32)), (S, B, tau, pi)
+                checked += 1
+    assert checked == len(d["n"])
+
+
+def test_search_matches_oracle_random_positions(gpu, oracle_lib):
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 384, seed=5)
+    bs = gpu.BatchedSearch(len(roots), 400)
+    ev = gpu.HashEvaluator(bs.engine)
+    for (S, B) in [(50, 8), (200, 4), (400, 8), (33, 5)]:
+        bs.run(roots, ev, S, B)
+        visits, L = bs.visits()
+        for i, s in enumerate(ostates):
+            _, vi, _ = core.pv_mcts_scores_hash(s, 1.0, S, B)
+            assert L[i] == vi.size
+            assert np.array_equal(visits[i, :L[i]], vi), (S, B, i)
+            assert visits[i].sum() == S
+
+
+def test_selfplay_matches_reference_driver(gpu):
+    """Golden games = reference self_play_cpp.play after np.random.seed(1234 + g)."""
+    d = golden("selfplay.npz")
+    ng = len(d["lengths"])
+    for slots in (5, 16):
+        sp = gpu.SelfPlay(slots, 50, 8, 1.0)
+        sp.run(0, ng, int(d["seeds"][0]))
+        recs = sp.records()
+        assert [r["game"] for r in recs] == list(range(ng))
+        off = 0
+        for g, r in enumerate(recs):
+            ln = int(d["lengths"][g])
+            sl = slice(off, off + ln)
+            assert len(r["actions"]) == ln
+            assert np.array_equal(r["actions"], d["actions"][sl].astype(np.int64))
+            assert np.array_equal(r["policies"].view(np.uint64), d["policies"][sl].view(np.uint64))
+            assert np.array_equal(r["values"], d["values"][sl].astype(np.int64))
+            assert np.array_equal(r["inputs"].reshape(ln, 243), d["tensors"][sl].astype(np.float32))
+            off += ln
+
+
+def test_selfplay_matches_oracle_and_is_slot_invariant(gpu, oracle_lib):
+    core = oracle_lib
+    n_games, seed = 24, 777
+    ref = [core.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
+    for slots in (1, 7, 32):
+        sp = gpu.SelfPlay(slots, 30, 4, 1.0)
+        sp.run(0, n_games, seed)
+        recs = sp.records()
+        assert len(recs) == n_games
+        for g, r in enumerate(recs):
+            assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (slots, g)
+            assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64))
+            assert np.array_equal(r["values"], ref[g]["values"].astype(np.int64))
+
+
+def test_play_uses_and_advances_global_numpy_rng(gpu):
+    import self_play_cpp
+    from oracle.hashnp import make_hash_model
+    d = golden("selfplay.npz")
+    model = make_hash_model()
+    off = 0
+    for g in range(3):
+        np.random.seed(int(d["seeds"][g]))
+        h = self_play_cpp.play(model)
+        ln = int(d["lengths"][g])
+        assert len(h) == ln
+        for i in range(ln):
+            assert np.array_equal(np.asarray(h[i][1]).view(np.uint64), d["policies"][off + i].view(np.uint64))
+            assert h[i][2] == d["values"][off + i]
+            assert h[i][0].shape == (9, 9, 3)
+        # one random_sample() (two MT words) per ply, exactly like np.random.choice
+        ref = np.random.RandomState(int(d["seeds"][g]))
+        for _ in range(ln):
+            ref.random_sample()
+        assert np.random.get_state()[2] == ref.get_state()[2]
+        assert np.array_equal(np.random.get_state()[1], ref.get_state()[1])
+        off += ln
+
+
+def test_uttt_cpp_callback_search_matches_golden(gpu):
+    import uttt_cpp
+    from oracle.hashnp import hash_eval_np
+    d = golden("search.npz")
+    calls = []
+
+    def model(states):
+        calls.append(len(states))
+        out = []
+        for s in states:
+            x = np.asarray(s.to_input_tensor(), np.float32).reshape(9, 9, 3).transpose(2, 0, 1)
+            p, v = hash_eval_np(x)
+            out.append((p, float(v)))
+        return out
+
+    rows = np.nonzero(((d["sims"] == 50) & (d["batch"] == 8)) | ((d["sims"] == 30) & (d["batch"] == 3)))[0]
+    for dedup in (True, False):
+        for r in rows[::2]:
+            i = int(d["pos"][r])
+            st = uttt_cpp.State(d["pos_pieces"][i].reshape(9, 9).tolist(), d["pos_enemy"][i].reshape(9, 9).tolist(),
+                                d["pos_main_p"][i].tolist(), d["pos_main_e"][i].tolist(), int(d["pos_active"][i]))
+            calls.clear()
+            sc = np.asarray(uttt_cpp.pv_mcts_scores(model=model, state=st, temperature=float(d["temp"][r]),
+                                                    evaluate_count=int(d["sims"][r]), batch_size=int(d["batch"][r]),
+                                                    dedup=dedup), np.float32)
+            n = int(d["n"][r])
+            assert np.array_equal(sc.view(np.uint32), d["scores"][r][:n].view(np.uint32))
+            assert len(calls) == d["flushes"][r]
+            if not dedup:
+                assert sum(calls) == d["evals"][r]
+
+
+def test_network_gpu_matches_cpu_fp32(gpu):
+    """NN value within 1e-5 (north star), policy within 1e-5; plain and BN-folded forms."""
+    import torch
+    from uttt_amd.model import FoldedDualNetwork, random_network
+    d = golden("network.npz")
+    cpu = random_network(0)
+    x = torch.from_numpy(d["x"])
+    with torch.no_grad():
+        p_ref, v_ref = cpu(x)
+    assert np.allclose(p_ref.numpy(), d["policy"], atol=1e-6) and np.allclose(v_ref.numpy(), d["value"], atol=1e-6)
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    rng = np.random.RandomState(0)
+    xr = torch.from_numpy((rng.rand(256, 3, 9, 9) < 0.3).astype(np.float32))
+    with torch.no_grad():
+        p_cpu, v_cpu = cpu(xr)
+    g = random_network(0, "cuda")
+    for net in (g, FoldedDualNetwork(g).to("cuda")):
+        with torch.no_grad():
+            p, v = net(xr.cuda())
+        assert (v.cpu() - v_cpu).abs().max().item() <= 1e-5
+        assert (p.cpu() - p_cpu).abs().max().item() <= 1e-5
+
+
+def test_nn_in_the_loop_search_replays_exactly(gpu, oracle_lib):
+    """Engine + real DualNetwork on the GPU; every (input -> output) pair the
+    network produced is replayed into the oracle: visit counts must be equal."""
+    import torch
+    from uttt_amd.model import random_network
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 64, seed=11)
+    net = random_network(0, "cuda")
+    table = {}
+
+    class Recording(gpu.NetworkEvaluator):
+        def __call__(self, x, n):
+            p, v = super().__call__(x, n)
+            xs = x[:n].cpu().numpy().reshape(n, 243)
+            ps, vs = p.cpu().numpy(), v.cpu().numpy().reshape(-1)
+            for i in range(n):
+                table[xs[i].tobytes()] = (ps[i].copy(), np.float32(vs[i]))
+            return p, v
+
+    bs = gpu.BatchedSearch(len(roots), 50)
+    bs.run(roots, Recording(net, len(roots)), 50, 8)
+    visits, L = bs.visits()
+
+    def replay(x):
+        return table[np.asarray(x, np.float32).reshape(243).tobytes()]
+
+    for i, s in enumerate(ostates):
+        _, vi, _ = core.pv_mcts_scores(s, 1.0, 50, 8, replay)
+        assert np.array_equal(visits[i, :L[i]], vi), i
+    assert torch.cuda.is_available()
+
+
+def test_full_size_4096x50_properties_and_samples(gpu, oracle_lib):
+    """BASELINE size (4096 trees x 50 sims, B=8): every root's visits sum to 50;
+    a sample of trees is bit-checked against the oracle."""
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 4096, seed=21)
+    bs = gpu.BatchedSearch(4096, 400)
+    ev = gpu.HashEvaluator(bs.engine)
+    for (S, B) in [(50, 8), (400, 8)]:
+        bs.run(roots, ev, S, B)
+        visits, L = bs.visits()
+        assert (visits.sum(axis=1) == S).all()
+        for i in range(0, 4096, 97):
+            _, vi, _ = core.pv_mcts_scores_hash(ostates[i], 1.0, S, B)
+            assert np.array_equal(visits[i, :L[i]], vi), (S, B, i)

@@ -1,0 +1,113 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports
+every function include/uttt_engine.h declares; the `uttt_cpp` State (bitboard
+rules shared with the kernels) reproduces the reference's rules, transitions,
+tensors and to_string on the golden fixtures; argument validation."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO, golden
+
+
+def _declared_functions():
+    with open(os.path.join(REPO, "include", "uttt_engine.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w]+\s*\*?\s*(uttt_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_abi_exports_every_declared_symbol(engine_lib):
+    names = _declared_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(engine_lib, n), n
+    assert engine_lib.uttt_version().decode().startswith("uttt-mi355x")
+
+
+def _st(m, d, i, prefix=""):
+    return m.State(d[prefix + "pieces"][i].reshape(9, 9).tolist(), d[prefix + "enemy"][i].reshape(9, 9).tolist(),
+                   d[prefix + "main_p"][i].tolist(), d[prefix + "main_e"][i].tolist(), int(d[prefix + "active"][i]))
+
+
+def test_state_rules_match_reference(uttt_cpp_mod):
+    m = uttt_cpp_mod
+    d = golden("rules.npz")
+    n = len(d["n_legal"])
+    for i in range(n):
+        s = _st(m, d, i)
+        assert s.legal_actions() == np.nonzero(d["legal"][i])[0].tolist()
+        fl = int(s.is_lose()) | int(s.is_draw()) << 1 | int(s.is_done()) << 2 | int(s.is_first_player()) << 3
+        assert fl == d["flags"][i]
+        assert np.array_equal(np.asarray(s.to_input_tensor(), np.float32), d["tensor"][i].astype(np.float32))
+        assert s.pieces == d["pieces"][i].reshape(9, 9).tolist()
+        assert s.main_board_enemy_pieces == d["main_e"][i].tolist()
+        a = int(d["action"][i])
+        if a >= 0 and i + 1 < n and d["game"][i + 1] == d["game"][i]:
+            nx = s.next(a)
+            assert nx.pieces == d["pieces"][i + 1].reshape(9, 9).tolist()
+            assert nx.enemy_pieces == d["enemy"][i + 1].reshape(9, 9).tolist()
+            assert nx.main_board_pieces == d["main_p"][i + 1].tolist()
+            assert nx.main_board_enemy_pieces == d["main_e"][i + 1].tolist()
+            assert nx.active_board == d["active"][i + 1]
+
+
+def test_unvalidated_next_matches_reference(uttt_cpp_mod):
+    m = uttt_cpp_mod
+    d = golden("rules.npz")
+    for i in range(len(d["odd_action"])):
+        nx = _st(m, d, i, "odd_").next(int(d["odd_action"][i]))
+        assert nx.pieces == d["odd_n_pieces"][i].reshape(9, 9).tolist()
+        assert nx.enemy_pieces == d["odd_n_enemy"][i].reshape(9, 9).tolist()
+        assert nx.main_board_pieces == d["odd_n_main_p"][i].tolist()
+        assert nx.main_board_enemy_pieces == d["odd_n_main_e"][i].tolist()
+        assert nx.active_board == d["odd_n_active"][i]
+
+
+def test_to_string_matches_reference(uttt_cpp_mod):
+    m = uttt_cpp_mod
+    with open(os.path.join(GOLDEN, "to_string.json")) as f:
+        items = json.load(f)
+    for it in items:
+        p, e, mp, me, a = it["state"]
+        s = m.State(np.reshape(p, (9, 9)).tolist(), np.reshape(e, (9, 9)).tolist(), mp, me, a)
+        assert s.to_string() == it["text"]
+        assert str(s) == it["text"]
+
+
+def test_state_validation_and_packing(uttt_cpp_mod):
+    m = uttt_cpp_mod
+    z = [[0] * 9 for _ in range(9)]
+    with pytest.raises(ValueError):
+        m.State([[2] * 9] + z[1:], z, [0] * 9, [0] * 9, -1)
+    with pytest.raises(ValueError):
+        m.State(z, z, [0] * 9, [0] * 9, 9)
+    with pytest.raises(TypeError):
+        m.State(z[:8], z, [0] * 9, [0] * 9, -1)
+    with pytest.raises(ValueError):
+        m.State().next(81)
+    s = m.State().next(40)
+    t = m.State.from_packed(s.packed)
+    assert t.pieces == s.pieces and t.active_board == 4 and len(s.packed) == 32
+
+
+def test_boltzman_matches_reference_values(uttt_cpp_mod, oracle_lib):
+    rng = np.random.RandomState(5)
+    for tau in (1.0, 0.5, 2.0, 0.25):
+        xs = rng.randint(0, 60, size=rng.randint(1, 82)).astype(np.float32)
+        a = np.asarray(uttt_cpp_mod.boltzman(xs.tolist(), tau), np.float32)
+        b = oracle_lib.boltzman(xs, tau)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_engine_requires_gpu_loudly():
+    """No silent CPU path: without a GPU the engine refuses to start."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from uttt_amd import Engine
+    from uttt_amd._lib import EngineError
+    with pytest.raises(EngineError):
+        Engine(4, 50)

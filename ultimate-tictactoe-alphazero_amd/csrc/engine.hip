@@ -1,0 +1,1452 @@
+// engine.hip — batched PV-MCTS + self-play for MI355X (gfx950, wave64).
+//
+// Many independent PUCT trees live in flat SoA pools in HBM:
+//   N[i] (i32 visits), W[i] (f32 value sum), P[i] (f32 prior), LINK[i] (uint2:
+//   first child | k copies : 16, |legal| : 8, action : 8)
+// indexed t * cap + local, the root at local 0. A node's children are one
+// contiguous block of k*|legal| entries (k = copies of the flushed leaf,
+// uttt_mcts.cpp:121-135 + :38-43 append semantics), so PUCT reads 12 B per
+// child fully coalesced. States are never stored per node: a descent replays
+// the actions from the root on bitboards (uttt_bits.h).
+//
+// One round (uttt_mcts.cpp:109-167, all trees in lock-step):
+//   k_select  one wave per tree: descend by PUCT (wave arg-max, first index
+//             wins ties), back up terminal simulations in place, stop at the
+//             first unexpanded leaf -> pending record (node, path, k).
+//   k_scan    one block: pending flags -> dense slots in tree order.
+//   k_encode  one thread per input element: leaf -> NCHW (3,9,9) f32 row.
+//   (evaluator: DualNetwork under PyTorch-ROCm, or k_hash_eval)
+//   k_apply   one wave per pending leaf: legal-mask + sequential f32
+//             renormalisation, k child blocks, k back-ups along the path.
+// Self-play (self_play_cpp.py) adds k_move_end (scores, f64 policy target,
+// numpy-legacy MT19937 choice, records), k_finalize (refill + arena offsets)
+// and k_archive.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "uttt_bits.h"
+#include "uttt_engine.h"
+
+namespace uttt {
+
+// ------------------------------------------------------------------ errors --
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return UTTT_ERR_HIP;                                                             \
+        }                                                                                    \
+    } while (0)
+
+// ------------------------------------------------------------------ layout --
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kMaxDepth = 128;  // path slots: lane d holds path[d] and path[64 + d]
+constexpr int kMaxPlies = 81;   // a game fills at most every cell
+constexpr int kNone = 0x7fffffff;
+
+constexpr int32_t kLive = 1;
+constexpr int32_t kErrCapacity = 2;
+constexpr int32_t kErrDepth = 4;
+constexpr int32_t kErrSelect = 8;
+constexpr int32_t kErrMask = kErrCapacity | kErrDepth | kErrSelect;
+
+enum KernelId { kKSelect = 0, kKApply, kKEncode, kKScan, kKMoveEnd, kKHash, kKernelCount };
+
+struct TreeCtl {
+    int32_t sims_done;
+    int32_t node_count;
+    int32_t status;
+    int32_t pad;
+};
+
+struct LeafRec {
+    int32_t node;
+    int32_t depth;
+    int32_t k;
+    int32_t pad;
+};
+
+struct Pool {
+    int32_t *n;
+    float *w;
+    float *p;
+    uint2 *link;
+    int64_t cap;
+};
+
+struct Trees {
+    TreeCtl *ctl;
+    uttt_state_t *root;
+    uttt_state_t *leaf;
+    LeafRec *rec;
+    int32_t *path;    // [tree][kMaxDepth]
+    int32_t *pending; // [tree]
+    int32_t *tree_of; // [slot]
+    int32_t *count;   // [1] pending leaves this round
+    int32_t n_trees;
+    int32_t sims;
+    int32_t batch;
+};
+
+// link.y packing
+__host__ __device__ __forceinline__ uint32_t pack_meta(uint32_t k, uint32_t L, uint32_t action) {
+    return (k & 0xFFFFu) | ((L & 0xFFu) << 16) | ((action & 0xFFu) << 24);
+}
+__host__ __device__ __forceinline__ int meta_k(uint32_t y) { return (int)(y & 0xFFFFu); }
+__host__ __device__ __forceinline__ int meta_L(uint32_t y) { return (int)((y >> 16) & 0xFFu); }
+__host__ __device__ __forceinline__ int meta_action(uint32_t y) { return (int)(y >> 24); }
+
+// ------------------------------------------------------------ wave helpers --
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+
+__device__ __forceinline__ uint64_t lanes_below() {
+    const int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Wave-wide arg-max: larger value wins, equal values -> smaller index
+// (the reference's strict '>' scan in child order, uttt_mcts.cpp:69-78).
+__device__ __forceinline__ void wave_argmax(float &v, int &i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(v, off);
+        const int oi = __shfl_xor(i, off);
+        if (ov > v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Orders this wave's global stores before its later global loads (other lanes
+// read what one lane wrote; same CU, so workgroup scope suffices).
+__device__ __forceinline__ void wave_memory_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// ----------------------------------------------------------- root (begin) --
+// uttt_mcts.cpp:92-103: root expanded at once with uniform priors 1.0f/|legal|.
+// Self-play passes `live` (slot flags); search passes nullptr (all live).
+__global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const uttt_state_t *src, const int32_t *live) {
+    const int lane = lane_id();
+    const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (t >= tr.n_trees) return;
+    const bool on = live ? (live[t] != 0) : true;
+    const uttt_state_t s = src[t];
+    const size_t base = (size_t)t * pool.cap;
+    uint32_t m[3];
+    legal_mask(s, m);
+    const bool l0 = on && bit_of(m, lane);
+    const bool l1 = on && lane < 17 && bit_of(m, 64 + lane);
+    const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
+    const int L = __popcll(b0) + __popcll(b1);
+    const float up = L ? 1.0f / (float)L : 0.0f;
+    if (l0) {
+        const int i = 1 + __popcll(b0 & lanes_below());
+        pool.n[base + i] = 0;
+        pool.w[base + i] = 0.0f;
+        pool.p[base + i] = up;
+        pool.link[base + i] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
+    }
+    if (l1) {
+        const int i = 1 + __popcll(b0) + __popcll(b1 & lanes_below());
+        pool.n[base + i] = 0;
+        pool.w[base + i] = 0.0f;
+        pool.p[base + i] = up;
+        pool.link[base + i] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
+    }
+    if (lane == 0) {
+        pool.n[base] = 0;
+        pool.w[base] = 0.0f;
+        pool.p[base] = 0.0f;
+        pool.link[base] = make_uint2(L ? 1u : 0u, pack_meta(L ? 1 : 0, (uint32_t)L, 0xFFu));
+        tr.root[t] = s;
+        TreeCtl c;
+        c.sims_done = 0;
+        c.node_count = 1 + L;
+        c.status = (on && L > 0) ? kLive : 0;
+        c.pad = 0;
+        tr.ctl[t] = c;
+    }
+}
+
+// --------------------------------------------------------------- select --
+// One wave per tree. uttt_mcts.cpp:109-127 for the simulations up to (and
+// including) the next one that reaches an unexpanded non-terminal leaf.
+// Terminal simulations are backed up in place (:115-118). The k-1 further
+// simulations the reference spends re-finding the same queued leaf are
+// accounted by k.
+__global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, unsigned long long *bytes_ctr) {
+    const int lane = lane_id();
+    const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (t >= tr.n_trees) return;
+    TreeCtl ctl = tr.ctl[t];
+    int pend = 0;
+    unsigned long long bytes = 0;
+    if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
+        const size_t base = (size_t)t * pool.cap;
+        int32_t *__restrict__ N = pool.n + base;
+        float *__restrict__ W = pool.w + base;
+        const float *__restrict__ P = pool.p + base;
+        const uint2 *__restrict__ LK = pool.link + base;
+        const uttt_state_t root = tr.root[t];
+        int sims_done = ctl.sims_done;
+        for (;;) {
+            uttt_state_t s = root;
+            int node = 0, depth = 0;
+            int path_lo = 0, path_hi = 0;  // lane d: path[d], path[64 + d]
+            uint2 lk = LK[0];
+            bool fail = false;
+            for (;;) {
+                const int cnt = meta_k(lk.y) * meta_L(lk.y);
+                if (cnt == 0) break;
+                const int first = (int)lk.x;
+                const int kself = node == 0 ? 0 : meta_k(lk.y);
+                const int total = N[node] - kself;  // == sum of children's visits
+                const float sq = sqrtf((float)total);
+                float best = -1e9f;
+                int bi = kNone;
+                for (int c = lane; c < cnt; c += kWave) {
+                    const int cn = N[first + c];
+                    const float cw = W[first + c];
+                    const float cp = P[first + c];
+                    // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off)
+                    const float q = (cn > 0) ? (-cw / (float)cn) : 0.0f;
+                    const float u = cp * sq / (float)(1 + cn);
+                    const float v = q + u;
+                    if (v > best) {
+                        best = v;
+                        bi = c;
+                    }
+                }
+                wave_argmax(best, bi);
+                bi = __builtin_amdgcn_readfirstlane(bi);
+                bytes += 12ull * (unsigned long long)cnt + 8ull;
+                if (bi == kNone) {  // every child NaN: the reference would dereference null
+                    fail = true;
+                    if (lane == 0) ctl.status |= kErrSelect;
+                    break;
+                }
+                node = first + bi;
+                ++depth;
+                if (depth >= kMaxDepth) {
+                    fail = true;
+                    if (lane == 0) ctl.status |= kErrDepth;
+                    break;
+                }
+                if (lane == (depth & 63)) {
+                    if (depth < 64) path_lo = node;
+                    else path_hi = node;
+                }
+                lk = LK[node];
+                s = next_state(s, meta_action(lk.y));
+            }
+            if (fail) break;
+            const bool lose = is_lose(s);
+            if (lose || legal_count(s) == 0u) {
+                // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
+                // backpropagate adds it at the leaf and flips sign upwards (:47-54).
+                const float v = -(lose ? -1.0f : 0.0f);
+                if (lane <= depth) {
+                    const float x = ((depth - lane) & 1) ? -v : v;
+                    W[path_lo] += x;
+                    N[path_lo] += 1;
+                }
+                if (lane + 64 <= depth) {
+                    const float x = ((depth - lane - 64) & 1) ? -v : v;
+                    W[path_hi] += x;
+                    N[path_hi] += 1;
+                }
+                wave_memory_fence();
+                bytes += 16ull * (unsigned long long)(depth + 1);
+                ++sims_done;
+                if (sims_done >= tr.sims) break;
+                continue;
+            }
+            // Unexpanded leaf (n == 0 && no children, uttt_mcts.cpp:121): queue it with
+            // k = the copies the reference would queue before flushing (:127).
+            const int k = min(tr.batch, tr.sims - sims_done);
+            int32_t *gp = tr.path + (size_t)t * kMaxDepth;
+            if (lane <= depth) gp[lane] = path_lo;
+            if (lane + 64 <= depth) gp[lane + 64] = path_hi;
+            if (lane == 0) {
+                LeafRec r;
+                r.node = node;
+                r.depth = depth;
+                r.k = k;
+                r.pad = 0;
+                tr.rec[t] = r;
+                tr.leaf[t] = s;
+            }
+            pend = 1;
+            break;
+        }
+        ctl.sims_done = sims_done;
+        if (lane == 0) tr.ctl[t] = ctl;
+    }
+    if (lane == 0) {
+        tr.pending[t] = pend;
+        if (bytes_ctr && bytes) atomicAdd(bytes_ctr, bytes);
+    }
+}
+
+// ------------------------------------------------------------------- scan --
+// One block: exclusive scan of pending flags -> tree_of[slot] in tree order.
+__global__ __launch_bounds__(1024) void k_scan(Trees tr) {
+    __shared__ int sums[1024];
+    const int tid = threadIdx.x;
+    const int per = (tr.n_trees + 1023) / 1024;
+    const int b = tid * per, e = min(b + per, tr.n_trees);
+    int local = 0;
+    for (int i = b; i < e; ++i) local += tr.pending[i];
+    sums[tid] = local;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int v = tid >= off ? sums[tid - off] : 0;
+        __syncthreads();
+        sums[tid] += v;
+        __syncthreads();
+    }
+    int slot = sums[tid] - local;
+    for (int i = b; i < e; ++i)
+        if (tr.pending[i]) tr.tree_of[slot++] = i;
+    if (tid == 1023) tr.count[0] = sums[1023];
+}
+
+// ----------------------------------------------------------------- encode --
+// The network input of each pending leaf (uttt_game.cpp:244-280 transposed to
+// NCHW as pv_mcts_cpp.py:57-60 does): ch0 own stones, ch1 opponent, ch2 legal.
+__global__ __launch_bounds__(256) void k_encode(Trees tr, float *__restrict__ x, int n) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * 243) return;
+    const int slot = g / 243, j = g % 243;
+    const int ch = j / 81, pos = j % 81;
+    const uttt_state_t s = tr.leaf[tr.tree_of[slot]];
+    const int a = action_at(pos);
+    uint32_t bit;
+    if (ch == 0) bit = bit_of(s.own, a);
+    else if (ch == 1) bit = bit_of(s.opp, a);
+    else {
+        uint32_t m[3];
+        legal_mask(s, m);
+        bit = bit_of(m, a);
+    }
+    x[g] = bit ? 1.0f : 0.0f;
+}
+
+// ------------------------------------------------------------------ apply --
+// One wave per pending leaf (uttt_mcts.cpp:138-167 for each of its k copies):
+// legal priors, sequential f32 sum in action order, divide (uniform 1/|legal|
+// if sum <= 0), append the child block, back up the value along the path.
+// per_copy: row rowbase[slot] + j holds copy j's result; else row = slot.
+__global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, const float *__restrict__ policy,
+                                                  int64_t pld, const float *__restrict__ value, int64_t vld,
+                                                  const int32_t *__restrict__ rowbase, int per_copy,
+                                                  unsigned long long *bytes_ctr) {
+    const int lane = lane_id();
+    const int slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (slot >= tr.count[0]) return;
+    const int t = tr.tree_of[slot];
+    const LeafRec r = tr.rec[t];
+    TreeCtl ctl = tr.ctl[t];
+    const uttt_state_t s = tr.leaf[t];
+    const size_t base = (size_t)t * pool.cap;
+    uint32_t m[3];
+    legal_mask(s, m);
+    const bool l0 = bit_of(m, lane) != 0u;
+    const bool l1 = lane < 17 && bit_of(m, 64 + lane) != 0u;
+    const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
+    const int L = __popcll(b0) + __popcll(b1);
+    const int i0 = __popcll(b0 & lanes_below());
+    const int i1 = __popcll(b0) + __popcll(b1 & lanes_below());
+    const int k = r.k;
+    const int nb = ctl.node_count;
+    if ((int64_t)nb + (int64_t)k * L > pool.cap || L == 0) {
+        if (lane == 0) {
+            ctl.status |= kErrCapacity;
+            tr.ctl[t] = ctl;
+        }
+        return;
+    }
+    const int depth = r.depth;
+    const int32_t *gp = tr.path + (size_t)t * kMaxDepth;
+    const int pn_lo = lane <= depth ? gp[lane] : 0;
+    const int pn_hi = lane + 64 <= depth ? gp[lane + 64] : 0;
+    float w_lo = lane <= depth ? pool.w[base + pn_lo] : 0.0f;
+    float w_hi = lane + 64 <= depth ? pool.w[base + pn_hi] : 0.0f;
+    const int copies = per_copy ? k : 1;
+    for (int j = 0; j < copies; ++j) {
+        const int64_t row = per_copy ? (int64_t)rowbase[slot] + j : (int64_t)slot;
+        const float *pol = policy + row * pld;
+        const float p0 = l0 ? pol[lane] : 0.0f;
+        const float p1 = l1 ? pol[64 + lane] : 0.0f;
+        // sequential f32 sum over legal actions in ascending order (uttt_mcts.cpp:144-152)
+        float sum = 0.0f;
+        for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
+        for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+        const float un = 1.0f / (float)L;
+        const float q0 = sum > 0 ? p0 / sum : un;
+        const float q1 = sum > 0 ? p1 / sum : un;
+        const int reps = per_copy ? 1 : k;
+        for (int rj = 0; rj < reps; ++rj) {
+            const int blk = nb + (j + rj) * L;
+            if (l0) {
+                pool.n[base + blk + i0] = 0;
+                pool.w[base + blk + i0] = 0.0f;
+                pool.p[base + blk + i0] = q0;
+                pool.link[base + blk + i0] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
+            }
+            if (l1) {
+                pool.n[base + blk + i1] = 0;
+                pool.w[base + blk + i1] = 0.0f;
+                pool.p[base + blk + i1] = q1;
+                pool.link[base + blk + i1] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
+            }
+        }
+        // backpropagate (uttt_mcts.cpp:47-54) this copy's value
+        const float v = value[row * vld];
+        const int reps_b = per_copy ? 1 : k;
+        for (int rj = 0; rj < reps_b; ++rj) {
+            if (lane <= depth) w_lo += ((depth - lane) & 1) ? -v : v;
+            if (lane + 64 <= depth) w_hi += ((depth - lane - 64) & 1) ? -v : v;
+        }
+    }
+    if (lane <= depth) {
+        pool.w[base + pn_lo] = w_lo;
+        pool.n[base + pn_lo] += k;
+    }
+    if (lane + 64 <= depth) {
+        pool.w[base + pn_hi] = w_hi;
+        pool.n[base + pn_hi] += k;
+    }
+    if (lane == 0) {
+        const uint2 old = pool.link[base + r.node];
+        pool.link[base + r.node] = make_uint2((uint32_t)nb, pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y)));
+        ctl.node_count = nb + k * L;
+        ctl.sims_done += k;
+        tr.ctl[t] = ctl;
+        if (bytes_ctr) {
+            const unsigned long long b = 20ull * (unsigned long long)(k * L) + 81ull * 4ull * copies + 4ull * copies +
+                                         8ull + 16ull * (unsigned long long)(depth + 1);
+            atomicAdd(bytes_ctr, b);
+        }
+    }
+}
+
+// -------------------------------------------------------------- hash eval --
+// Deterministic test evaluator on the NCHW rows: one wave per row; the 4
+// ballots of "x != 0" over the 243 floats are exactly the 4 hash words.
+__global__ __launch_bounds__(kBlock) void k_hash_eval(const float *__restrict__ x, int n, float *__restrict__ policy,
+                                                      float *__restrict__ value) {
+    const int lane = lane_id();
+    const int row = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const float *xr = x + (size_t)row * 243;
+    uint64_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = i * 64 + lane;
+        w[i] = __ballot(j < 243 && xr[j] != 0.0f);
+    }
+    const uint64_t h = hash_words(w);
+    policy[(size_t)row * 81 + lane] = hash_prior(h, lane);
+    if (lane < 17) policy[(size_t)row * 81 + 64 + lane] = hash_prior(h, 64 + lane);
+    if (lane == 0) value[row] = hash_value(h);
+}
+
+// ---------------------------------------------------------- root results --
+__device__ __forceinline__ int root_children(const Pool &pool, size_t base, int &first) {
+    const uint2 lk = pool.link[base];
+    first = (int)lk.x;
+    return meta_L(lk.y);
+}
+
+// pv_mcts_scores' return value (uttt_mcts.cpp:177-195): root child visits as
+// f32 -> one-hot first max (t == 0) or boltzman (:199-216).
+__device__ void root_scores(const Pool &pool, size_t base, float temperature, float *sc, int &L) {
+    int first;
+    L = root_children(pool, base, first);
+    if (temperature == 0.0f) {
+        int mi = 0;
+        float mv = L ? (float)pool.n[base + first] : 0.0f;
+        for (int i = 1; i < L; ++i) {
+            const float v = (float)pool.n[base + first + i];
+            if (v > mv) {
+                mv = v;
+                mi = i;
+            }
+        }
+        for (int i = 0; i < L; ++i) sc[i] = (i == mi) ? 1.0f : 0.0f;
+    } else {
+        float sum = 0.0f;
+        for (int i = 0; i < L; ++i) {
+            sc[i] = powf((float)pool.n[base + first + i], 1.0f / temperature);
+            sum += sc[i];
+        }
+        if (sum > 0)
+            for (int i = 0; i < L; ++i) sc[i] /= sum;
+    }
+}
+
+__global__ void k_root_visits(Pool pool, Trees tr, int32_t *visits, int32_t *n_legal) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tr.n_trees * 81) return;
+    const int t = g / 81, i = g % 81;
+    const size_t base = (size_t)t * pool.cap;
+    int first;
+    const int L = root_children(pool, base, first);
+    visits[g] = i < L ? pool.n[base + first + i] : 0;
+    if (i == 0) n_legal[t] = L;
+}
+
+__global__ void k_root_scores(Pool pool, Trees tr, float temperature, float *scores, int32_t *n_legal) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= tr.n_trees) return;
+    float sc[81];
+    int L;
+    root_scores(pool, (size_t)t * pool.cap, temperature, sc, L);
+    for (int i = 0; i < 81; ++i) scores[(size_t)t * 81 + i] = i < L ? sc[i] : 0.0f;
+    n_legal[t] = L;
+}
+
+// -------------------------------------------------------------- self-play --
+struct Slot {
+    uttt_state_t state;
+    int64_t game;        // game id being played (-1: none)
+    int32_t ply;
+    int32_t live;
+    int32_t finished;    // set by k_move_end when the game just ended
+    int32_t fin_len;
+    int64_t fin_game;
+    int64_t fin_offset;  // arena row of its first ply
+    int32_t fin_value;   // value of ply 0 (self_play_cpp.py:95)
+    int32_t pad;
+};
+
+struct GameEntry {
+    int64_t game;
+    int64_t offset;
+    int64_t length;
+};
+
+struct SelfPlay {
+    Slot *slot;
+    uint32_t *mt_key;      // [slot][624]
+    int32_t *mt_pos;       // [slot]
+    uttt_state_t *ply_state;  // [slot][81]
+    double *ply_policy;    // [slot][81][81]
+    int8_t *ply_action;    // [slot][81]
+    uttt_state_t *ar_state;
+    double *ar_policy;
+    int8_t *ar_action;
+    int8_t *ar_value;
+    GameEntry *games;
+    int64_t *ctr;          // [0] next game id, [1] games finished, [2] arena plies used
+    int32_t *live;         // [slot] flags for k_begin
+    int64_t game_end;
+    int64_t arena_cap;
+    int64_t games_cap;
+    uint32_t seed_base;
+    float temperature;
+    int32_t slots;
+};
+
+// numpy legacy RandomState: init_genrand(seed) (mt19937_seed), genrand_int32
+// with the standard twist/tempering, random_sample = 53-bit double of 2 draws.
+__device__ void mt_seed(uint32_t *key, int32_t *pos, uint32_t seed) {
+    key[0] = seed;
+    for (int i = 1; i < 624; ++i) key[i] = 1812433253u * (key[i - 1] ^ (key[i - 1] >> 30)) + (uint32_t)i;
+    *pos = 624;
+}
+
+__device__ uint32_t mt_next32(uint32_t *key, int32_t *pos) {
+    if (*pos >= 624) {
+        for (int i = 0; i < 624; ++i) {
+            const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1 < 624 ? i + 1 : 0] & 0x7fffffffu);
+            uint32_t v = key[i + 397 < 624 ? i + 397 : i + 397 - 624] ^ (y >> 1);
+            if (y & 1u) v ^= 0x9908b0dfu;
+            key[i] = v;
+        }
+        *pos = 0;
+    }
+    uint32_t y = key[(*pos)++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+__device__ double mt_double(uint32_t *key, int32_t *pos) {
+    const uint32_t a = mt_next32(key, pos) >> 5, b = mt_next32(key, pos) >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+// np.add.reduce on a contiguous float64 vector (pairwise, 8 accumulators, blocks <= 128).
+__device__ double np_sum(const double *a, int n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;  // n <= 81 < 128: a single pairwise block
+}
+
+// One thread per slot: the per-move tail of self_play_cpp.play (:63-92).
+__global__ void k_move_end(Pool pool, SelfPlay sp) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= sp.slots) return;
+    Slot sl = sp.slot[s];
+    sl.finished = 0;
+    if (!sl.live) {
+        sp.slot[s] = sl;
+        return;
+    }
+    const size_t base = (size_t)s * pool.cap;
+    float sc[81];
+    int L;
+    root_scores(pool, base, sp.temperature, sc, L);
+    // scores -> float64, renormalised with np.sum (:74-78)
+    double d[81];
+    for (int i = 0; i < L; ++i) d[i] = (double)sc[i];
+    const double tot = np_sum(d, L);
+    if (tot == 0.0) {
+        for (int i = 0; i < L; ++i) d[i] = 1.0 / (double)L;
+    } else {
+        for (int i = 0; i < L; ++i) d[i] = d[i] / tot;
+    }
+    // legal actions (ascending) of the root
+    uint32_t m[3];
+    legal_mask(sl.state, m);
+    int8_t leg[81];
+    int nl = 0;
+    for (int w = 0; w < 3; ++w)
+        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) leg[nl++] = (int8_t)(27 * w + __builtin_ctz(bits));
+    // policy target (:81-83) into the slot's ply buffer
+    const int ply = sl.ply;
+    double *pt = sp.ply_policy + ((size_t)s * kMaxPlies + ply) * 81;
+    for (int a = 0; a < 81; ++a) pt[a] = 0.0;
+    for (int i = 0; i < L; ++i) pt[leg[i]] = d[i];
+    // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right
+    double acc = 0.0;
+    for (int i = 0; i < L; ++i) {
+        acc += d[i];
+        d[i] = acc;
+    }
+    const double last = d[L - 1];
+    uint32_t *key = sp.mt_key + (size_t)s * 624;
+    const double u = mt_double(key, sp.mt_pos + s);
+    int idx = 0;
+    while (idx < L && d[idx] / last <= u) ++idx;
+    if (idx >= L) idx = L - 1;
+    const int action = leg[idx];
+    sp.ply_state[(size_t)s * kMaxPlies + ply] = sl.state;
+    sp.ply_action[(size_t)s * kMaxPlies + ply] = (int8_t)action;
+    sl.state = next_state(sl.state, action);
+    sl.ply = ply + 1;
+    if (is_done(sl.state) || sl.ply >= kMaxPlies) {
+        sl.finished = 1;
+        sl.fin_len = sl.ply;
+        sl.fin_game = sl.game;
+        sl.fin_value = is_lose(sl.state) ? -1 : 0;  // self_play_cpp.py:95
+        sl.live = 0;
+    }
+    sp.slot[s] = sl;
+}
+
+// One block: give finished games arena rows (slot order) and free slots the
+// next game ids (slot order) — deterministic for a given slot count.
+__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
+    __shared__ long long fin_sum[1024];
+    __shared__ int free_sum[1024];
+    const int tid = threadIdx.x;
+    const int per = (sp.slots + 1023) / 1024;
+    const int b = tid * per, e = min(b + per, sp.slots);
+    long long fl = 0;
+    int fr = 0, fc = 0;
+    for (int i = b; i < e; ++i) {
+        const Slot &sl = sp.slot[i];
+        if (sl.finished) {
+            fl += sl.fin_len;
+            ++fc;
+        }
+        if (!sl.live) ++fr;
+    }
+    fin_sum[tid] = fl;
+    free_sum[tid] = fr;
+    __shared__ int fcount[1024];
+    fcount[tid] = fc;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const long long a = tid >= off ? fin_sum[tid - off] : 0;
+        const int c = tid >= off ? free_sum[tid - off] : 0;
+        const int d = tid >= off ? fcount[tid - off] : 0;
+        __syncthreads();
+        fin_sum[tid] += a;
+        free_sum[tid] += c;
+        fcount[tid] += d;
+        __syncthreads();
+    }
+    const int64_t arena0 = sp.ctr[2], games0 = sp.ctr[1], next0 = sp.ctr[0];
+    long long off = arena0 + fin_sum[tid] - fl;
+    int gi = (int)(games0 + fcount[tid] - fc);
+    int fi = free_sum[tid] - fr;
+    for (int i = b; i < e; ++i) {
+        Slot sl = sp.slot[i];
+        if (sl.finished) {
+            if (off + sl.fin_len <= sp.arena_cap && gi < sp.games_cap) {
+                sl.fin_offset = off;
+                GameEntry ge;
+                ge.game = sl.fin_game;
+                ge.offset = off;
+                ge.length = sl.fin_len;
+                sp.games[gi] = ge;
+            } else {
+                sl.fin_offset = -1;  // arena full: host reports UTTT_ERR_CAPACITY
+            }
+            off += sl.fin_len;
+            ++gi;
+        }
+        if (!sl.live) {
+            const int64_t g = next0 + fi;
+            ++fi;
+            if (g < sp.game_end) {
+                sl.state.own[0] = sl.state.own[1] = sl.state.own[2] = 0u;
+                sl.state.opp[0] = sl.state.opp[1] = sl.state.opp[2] = 0u;
+                sl.state.mains = 0u;
+                sl.state.active = -1;
+                sl.game = g;
+                sl.ply = 0;
+                sl.live = 1;
+                mt_seed(sp.mt_key + (size_t)i * 624, sp.mt_pos + i, sp.seed_base + (uint32_t)g);
+            } else {
+                sl.game = -1;
+            }
+        }
+        sp.live[i] = sl.live;
+        sp.slot[i] = sl;
+    }
+    __syncthreads();
+    if (tid == 1023) {
+        sp.ctr[2] = arena0 + fin_sum[1023];
+        sp.ctr[1] = games0 + fcount[1023];
+        const int64_t nxt = next0 + free_sum[1023];
+        sp.ctr[0] = nxt < sp.game_end ? nxt : sp.game_end;
+    }
+}
+
+// Copy each just-finished game's plies to its arena rows, with values
+// (self_play_cpp.py:95-99: ply 0 gets the final value, then alternating).
+__global__ void k_archive(SelfPlay sp) {
+    const int s = blockIdx.x;
+    const Slot &sl = sp.slot[s];
+    if (!sl.finished || sl.fin_offset < 0) return;
+    for (int i = threadIdx.x; i < sl.fin_len * 81; i += blockDim.x) {
+        const int ply = i / 81, a = i % 81;
+        const size_t src = (size_t)s * kMaxPlies + ply;
+        const size_t dst = (size_t)sl.fin_offset + ply;
+        sp.ar_policy[dst * 81 + a] = sp.ply_policy[src * 81 + a];
+        if (a == 0) {
+            sp.ar_state[dst] = sp.ply_state[src];
+            sp.ar_action[dst] = sp.ply_action[src];
+            sp.ar_value[dst] = (int8_t)((ply & 1) ? -sl.fin_value : sl.fin_value);
+        }
+    }
+}
+
+__global__ void k_hwc(const uttt_state_t *st, int64_t n, float *out) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * 81) return;
+    const int64_t row = g / 81;
+    const int a = (int)(g % 81);
+    const uttt_state_t s = st[row];
+    uint32_t m[3];
+    legal_mask(s, m);
+    float *o = out + row * 243 + image_index(a) * 3;
+    o[0] = bit_of(s.own, a) ? 1.0f : 0.0f;
+    o[1] = bit_of(s.opp, a) ? 1.0f : 0.0f;
+    o[2] = bit_of(m, a) ? 1.0f : 0.0f;
+}
+
+}  // namespace uttt
+
+// ============================================================== host side ==
+using namespace uttt;
+
+struct uttt_engine {
+    int device = 0;
+    int max_trees = 0;
+    int max_sims = 0;
+    int64_t cap = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    Pool pool{};
+    Trees tr{};
+    int32_t *h_count = nullptr;  // pinned
+    int32_t *d_rowbase = nullptr;
+    float *d_pol_scratch = nullptr;
+    float *d_val_scratch = nullptr;
+    int64_t scratch_rows = 0;
+    float *d_scores = nullptr;
+    int32_t *d_nlegal = nullptr;
+    int32_t *d_visits = nullptr;
+    int64_t bytes = 0;
+    // round state
+    int phase = 0;  // 0 idle, 1 search begun (select next), 2 selected (apply next)
+    int n_pending = 0;
+    bool selfplay = false;
+    // self-play
+    SelfPlay sp{};
+    int64_t sp_arena_used = 0;
+    // telemetry
+    bool timing = false;
+    unsigned long long *d_bytes = nullptr;  // [kKernelCount]
+    struct Ev {
+        int kid;
+        hipEvent_t a, b;
+    };
+    std::vector<Ev> pending_ev;
+    std::vector<hipEvent_t> ev_pool;
+    double ms[kKernelCount] = {};
+    int64_t launches[kKernelCount] = {};
+    std::vector<void *> allocs;
+};
+
+namespace {
+
+int dev_alloc(uttt_engine *e, void **p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t r = hipMalloc(p, bytes);
+    if (r != hipSuccess) {
+        set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(r));
+        return UTTT_ERR_HIP;
+    }
+    e->allocs.push_back(*p);
+    e->bytes += (int64_t)bytes;
+    return UTTT_OK;
+}
+
+template <typename T>
+int alloc_n(uttt_engine *e, T **p, size_t n) {
+    return dev_alloc(e, reinterpret_cast<void **>(p), n * sizeof(T));
+}
+
+hipEvent_t get_event(uttt_engine *e) {
+    if (!e->ev_pool.empty()) {
+        hipEvent_t ev = e->ev_pool.back();
+        e->ev_pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    return ev;
+}
+
+struct TimedLaunch {
+    uttt_engine *e;
+    int kid;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(uttt_engine *e_, int kid_) : e(e_), kid(kid_) {
+        e->launches[kid]++;
+        if (e->timing) {
+            a = get_event(e);
+            b = get_event(e);
+            if (a) (void)hipEventRecord(a, e->stream);
+        }
+    }
+    ~TimedLaunch() {
+        if (e->timing && a && b) {
+            (void)hipEventRecord(b, e->stream);
+            e->pending_ev.push_back({kid, a, b});
+        }
+    }
+};
+
+// Called after a stream sync: fold finished event pairs into the totals.
+void drain_events(uttt_engine *e) {
+    for (auto &ev : e->pending_ev) {
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, ev.a, ev.b) == hipSuccess) e->ms[ev.kid] += ms;
+        e->ev_pool.push_back(ev.a);
+        e->ev_pool.push_back(ev.b);
+    }
+    e->pending_ev.clear();
+}
+
+unsigned long long *bytes_ptr(uttt_engine *e, int kid) { return e->timing ? e->d_bytes + kid : nullptr; }
+
+int check_launch() {
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) {
+        set_error("kernel launch failed: %s", hipGetErrorString(r));
+        return UTTT_ERR_HIP;
+    }
+    return UTTT_OK;
+}
+
+int grid_waves(int waves) { return (waves + kWavesPerBlock - 1) / kWavesPerBlock; }
+
+int ensure_scratch(uttt_engine *e, int64_t rows) {
+    if (rows <= e->scratch_rows) return UTTT_OK;
+    int64_t n = e->scratch_rows ? e->scratch_rows : 1024;
+    while (n < rows) n *= 2;
+    if (e->d_pol_scratch) {
+        (void)hipFree(e->d_pol_scratch);
+        (void)hipFree(e->d_val_scratch);
+        (void)hipFree(e->d_rowbase);
+    }
+    HIP_TRY(hipMalloc((void **)&e->d_pol_scratch, (size_t)n * 81 * sizeof(float)));
+    HIP_TRY(hipMalloc((void **)&e->d_val_scratch, (size_t)n * sizeof(float)));
+    HIP_TRY(hipMalloc((void **)&e->d_rowbase, (size_t)std::max<int64_t>(n, e->max_trees) * sizeof(int32_t)));
+    e->scratch_rows = n;
+    return UTTT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *uttt_last_error(void) { return g_err.c_str(); }
+const char *uttt_version(void) { return "uttt-mi355x 0.1 (gfx950)"; }
+
+int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out) {
+    if (!out || max_trees <= 0 || max_sims <= 0 || max_sims > 60000) {
+        set_error("uttt_engine_create: bad arguments (max_trees=%d, max_sims=%d)", max_trees, max_sims);
+        return UTTT_ERR_ARG;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device visible");
+        return UTTT_ERR_NODEVICE;
+    }
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) device = 0;
+    if (device < 0 || device >= ndev) {
+        set_error("device %d out of range (%d visible)", device, ndev);
+        return UTTT_ERR_NODEVICE;
+    }
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error("device %d is %s; this engine is built for gfx950 (MI355X)", device, prop.gcnArchName);
+        return UTTT_ERR_NODEVICE;
+    }
+    HIP_TRY(hipSetDevice(device));
+    uttt_engine *e = new uttt_engine();
+    e->device = device;
+    e->max_trees = max_trees;
+    e->max_sims = max_sims;
+    e->cap = 82 + 81ll * max_sims;  // root + 81 children + 81 per consumed simulation (exact bound)
+    int rc = UTTT_OK;
+    auto fail = [&](int code) {
+        uttt_engine_destroy(e);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(UTTT_ERR_HIP);
+    e->stream = e->own_stream;
+    const size_t nodes = (size_t)max_trees * (size_t)e->cap;
+    e->pool.cap = e->cap;
+    if ((rc = alloc_n(e, &e->pool.n, nodes)) || (rc = alloc_n(e, &e->pool.w, nodes)) ||
+        (rc = alloc_n(e, &e->pool.p, nodes)) || (rc = alloc_n(e, &e->pool.link, nodes)))
+        return fail(rc);
+    if ((rc = alloc_n(e, &e->tr.ctl, max_trees)) || (rc = alloc_n(e, &e->tr.root, max_trees)) ||
+        (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
+        (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
+        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 1)) ||
+        (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
+        (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)))
+        return fail(rc);
+    if (hipHostMalloc((void **)&e->h_count, sizeof(int32_t) * 4, hipHostMallocDefault) != hipSuccess) {
+        set_error("hipHostMalloc failed");
+        return fail(UTTT_ERR_HIP);
+    }
+    if (hipMemsetAsync(e->tr.ctl, 0, sizeof(TreeCtl) * max_trees, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) {
+        set_error("engine init memset failed");
+        return fail(UTTT_ERR_HIP);
+    }
+    e->tr.n_trees = 0;
+    *out = e;
+    return UTTT_OK;
+}
+
+int uttt_engine_destroy(uttt_engine_t *e) {
+    if (!e) return UTTT_OK;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    drain_events(e);
+    for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+    for (void *p : e->allocs) (void)hipFree(p);
+    if (e->d_pol_scratch) (void)hipFree(e->d_pol_scratch);
+    if (e->d_val_scratch) (void)hipFree(e->d_val_scratch);
+    if (e->d_rowbase) (void)hipFree(e->d_rowbase);
+    if (e->h_count) (void)hipHostFree(e->h_count);
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    delete e;
+    return UTTT_OK;
+}
+
+int uttt_engine_set_stream(uttt_engine_t *e, void *stream) {
+    if (!e) return UTTT_ERR_ARG;
+    e->stream = stream ? (hipStream_t)stream : e->own_stream;
+    return UTTT_OK;
+}
+
+int64_t uttt_engine_device_bytes(const uttt_engine_t *e) { return e ? e->bytes : 0; }
+
+static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, int32_t batch) {
+    if (n_trees <= 0 || n_trees > e->max_trees) {
+        set_error("n_trees %d out of range 1..%d", n_trees, e->max_trees);
+        return UTTT_ERR_ARG;
+    }
+    if (sims <= 0 || sims > e->max_sims) {
+        set_error("evaluate_count %d out of range 1..%d (engine max_sims)", sims, e->max_sims);
+        return UTTT_ERR_ARG;
+    }
+    e->tr.n_trees = n_trees;
+    e->tr.sims = sims;
+    // uttt_mcts.cpp:127: a flush happens once the queue holds batch_size entries,
+    // so batch_size <= 1 flushes every queued leaf alone.
+    e->tr.batch = batch < 1 ? 1 : batch;
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
+}
+
+int uttt_search_begin(uttt_engine_t *e, const uttt_state_t *roots, int32_t n_trees, int32_t sims, int32_t batch) {
+    if (!e || !roots) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = search_begin_common(e, n_trees, sims, batch);
+    if (rc) return rc;
+    e->selfplay = false;
+    HIP_TRY(hipMemcpyAsync(e->tr.leaf, roots, sizeof(uttt_state_t) * n_trees, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_begin, dim3(grid_waves(n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+                       (const uttt_state_t *)e->tr.leaf, (const int32_t *)nullptr);
+    return check_launch();
+}
+
+int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
+    if (!e || !n_pending) return UTTT_ERR_ARG;
+    if (e->phase != 1) {
+        set_error("uttt_search_select: call uttt_search_begin (or apply the previous round) first");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    {
+        TimedLaunch tl(e, kKSelect);
+        hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+                           bytes_ptr(e, kKSelect));
+    }
+    int rc = check_launch();
+    if (rc) return rc;
+    {
+        TimedLaunch tl(e, kKScan);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr);
+    }
+    if ((rc = check_launch())) return rc;
+    HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    drain_events(e);
+    const int n = e->h_count[0];
+    if (n > 0 && nn_input) {
+        TimedLaunch tl(e, kKEncode);
+        const int total = n * 243;
+        hipLaunchKernelGGL(k_encode, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->tr, nn_input, n);
+    }
+    if ((rc = check_launch())) return rc;
+    e->n_pending = n;
+    e->phase = n > 0 ? 2 : 1;
+    *n_pending = n;
+    return UTTT_OK;
+}
+
+int uttt_search_pending(uttt_engine_t *e, uttt_state_t *states, int32_t *copies) {
+    if (!e) return UTTT_ERR_ARG;
+    if (e->phase != 2) {
+        set_error("uttt_search_pending: no pending leaves (call uttt_search_select)");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    const int n = e->n_pending;
+    std::vector<int32_t> tree_of(n);
+    HIP_TRY(hipMemcpyAsync(tree_of.data(), e->tr.tree_of, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+    std::vector<uttt_state_t> leaf(e->tr.n_trees);
+    std::vector<LeafRec> rec(e->tr.n_trees);
+    HIP_TRY(hipMemcpyAsync(leaf.data(), e->tr.leaf, sizeof(uttt_state_t) * e->tr.n_trees, hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipMemcpyAsync(rec.data(), e->tr.rec, sizeof(LeafRec) * e->tr.n_trees, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int i = 0; i < n; ++i) {
+        if (states) states[i] = leaf[tree_of[i]];
+        if (copies) copies[i] = rec[tree_of[i]].k;
+    }
+    return UTTT_OK;
+}
+
+int uttt_search_apply(uttt_engine_t *e, const float *policy, int64_t pld, const float *value, int64_t vld,
+                      int32_t per_copy, int32_t on_device) {
+    if (!e || !policy || !value || pld < 81 || vld < 1) {
+        set_error("uttt_search_apply: bad arguments (policy stride must be >= 81)");
+        return UTTT_ERR_ARG;
+    }
+    if (e->phase != 2) {
+        set_error("uttt_search_apply: no pending leaves (call uttt_search_select)");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    const int n = e->n_pending;
+    const int32_t *rowbase = nullptr;
+    int64_t rows = n;
+    if (per_copy) {
+        // rows are grouped per slot: slot i's k_i copies start at sum_{j<i} k_j
+        std::vector<int32_t> k(n);
+        int rc = uttt_search_pending(e, nullptr, k.data());
+        if (rc) return rc;
+        std::vector<int32_t> rb(n);
+        int64_t acc = 0;
+        for (int i = 0; i < n; ++i) {
+            rb[i] = (int32_t)acc;
+            acc += k[i];
+        }
+        rows = acc;
+        if ((rc = ensure_scratch(e, rows))) return rc;
+        HIP_TRY(hipMemcpyAsync(e->d_rowbase, rb.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+        rowbase = e->d_rowbase;
+    }
+    const float *dp = policy, *dv = value;
+    int64_t dpld = pld, dvld = vld;
+    if (!on_device) {
+        int rc = ensure_scratch(e, rows);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy2DAsync(e->d_pol_scratch, 81 * sizeof(float), policy, (size_t)pld * sizeof(float),
+                                 81 * sizeof(float), (size_t)rows, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipMemcpy2DAsync(e->d_val_scratch, sizeof(float), value, (size_t)vld * sizeof(float), sizeof(float),
+                                 (size_t)rows, hipMemcpyHostToDevice, e->stream));
+        dp = e->d_pol_scratch;
+        dv = e->d_val_scratch;
+        dpld = 81;
+        dvld = 1;
+    }
+    {
+        TimedLaunch tl(e, kKApply);
+        hipLaunchKernelGGL(k_apply, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, e->pool, e->tr, dp, dpld, dv, dvld,
+                           rowbase, per_copy ? 1 : 0, bytes_ptr(e, kKApply));
+    }
+    int rc = check_launch();
+    if (rc) return rc;
+    if (!on_device) HIP_TRY(hipStreamSynchronize(e->stream));  // host buffers may be freed on return
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
+}
+
+int uttt_eval_hash(uttt_engine_t *e, const float *nn_input, int32_t n, float *policy, float *value) {
+    if (!e || !nn_input || !policy || !value || n < 0) return UTTT_ERR_ARG;
+    if (n == 0) return UTTT_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    {
+        TimedLaunch tl(e, kKHash);
+        hipLaunchKernelGGL(k_hash_eval, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, nn_input, n, policy, value);
+    }
+    return check_launch();
+}
+
+static int check_tree_errors(uttt_engine *e) {
+    std::vector<TreeCtl> ctl(e->tr.n_trees);
+    HIP_TRY(hipMemcpyAsync(ctl.data(), e->tr.ctl, sizeof(TreeCtl) * e->tr.n_trees, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int t = 0; t < e->tr.n_trees; ++t) {
+        if (ctl[t].status & kErrMask) {
+            set_error("tree %d failed (status 0x%x: %s)", t, ctl[t].status,
+                      (ctl[t].status & kErrCapacity) ? "node pool exhausted"
+                      : (ctl[t].status & kErrDepth)  ? "path deeper than 128"
+                                                     : "no selectable child (NaN statistics)");
+            return (ctl[t].status & kErrSelect) ? UTTT_ERR_ARG : UTTT_ERR_CAPACITY;
+        }
+    }
+    return UTTT_OK;
+}
+
+int uttt_search_root_visits(uttt_engine_t *e, int32_t *visits, int32_t *n_legal) {
+    if (!e) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = check_tree_errors(e);
+    if (rc) return rc;
+    const int n = e->tr.n_trees;
+    hipLaunchKernelGGL(k_root_visits, dim3((n * 81 + 255) / 256), dim3(256), 0, e->stream, e->pool, e->tr, e->d_visits,
+                       e->d_nlegal);
+    if ((rc = check_launch())) return rc;
+    if (visits)
+        HIP_TRY(hipMemcpyAsync(visits, e->d_visits, sizeof(int32_t) * 81 * n, hipMemcpyDeviceToHost, e->stream));
+    if (n_legal) HIP_TRY(hipMemcpyAsync(n_legal, e->d_nlegal, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return UTTT_OK;
+}
+
+int uttt_search_scores(uttt_engine_t *e, float temperature, float *scores, int32_t *n_legal) {
+    if (!e) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = check_tree_errors(e);
+    if (rc) return rc;
+    const int n = e->tr.n_trees;
+    hipLaunchKernelGGL(k_root_scores, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->pool, e->tr, temperature,
+                       e->d_scores, e->d_nlegal);
+    if ((rc = check_launch())) return rc;
+    if (scores) HIP_TRY(hipMemcpyAsync(scores, e->d_scores, sizeof(float) * 81 * n, hipMemcpyDeviceToHost, e->stream));
+    if (n_legal) HIP_TRY(hipMemcpyAsync(n_legal, e->d_nlegal, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return UTTT_OK;
+}
+
+// ----------------------------------------------------------- self-play API --
+int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, uint32_t seed_base, float temperature,
+                        int32_t sims, int32_t batch, int64_t arena_plies) {
+    if (!e || game_end < game_begin || game_begin < 0 || arena_plies <= 0) {
+        set_error("uttt_selfplay_begin: bad arguments");
+        return UTTT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    const int slots = e->max_trees;
+    int rc = search_begin_common(e, slots, sims, batch);
+    if (rc) return rc;
+    e->phase = 0;  // move_begin first
+    SelfPlay &sp = e->sp;
+    if (!sp.slot) {
+        if ((rc = alloc_n(e, &sp.slot, slots)) || (rc = alloc_n(e, &sp.mt_key, (size_t)slots * 624)) ||
+            (rc = alloc_n(e, &sp.mt_pos, slots)) || (rc = alloc_n(e, &sp.ply_state, (size_t)slots * kMaxPlies)) ||
+            (rc = alloc_n(e, &sp.ply_policy, (size_t)slots * kMaxPlies * 81)) ||
+            (rc = alloc_n(e, &sp.ply_action, (size_t)slots * kMaxPlies)) || (rc = alloc_n(e, &sp.ctr, 4)) ||
+            (rc = alloc_n(e, &sp.live, slots)))
+            return rc;
+    }
+    // every archived game has >= 1 ply, so the arena bounds the game table too
+    const int64_t games = std::min<int64_t>(game_end - game_begin, arena_plies);
+    if (sp.arena_cap < arena_plies) {
+        if (sp.ar_state) {
+            (void)hipFree(sp.ar_state);
+            (void)hipFree(sp.ar_policy);
+            (void)hipFree(sp.ar_action);
+            (void)hipFree(sp.ar_value);
+        }
+        HIP_TRY(hipMalloc((void **)&sp.ar_state, sizeof(uttt_state_t) * arena_plies));
+        HIP_TRY(hipMalloc((void **)&sp.ar_policy, sizeof(double) * 81 * arena_plies));
+        HIP_TRY(hipMalloc((void **)&sp.ar_action, arena_plies));
+        HIP_TRY(hipMalloc((void **)&sp.ar_value, arena_plies));
+        sp.arena_cap = arena_plies;
+    }
+    if (sp.games_cap < games || !sp.games) {
+        if (sp.games) (void)hipFree(sp.games);
+        HIP_TRY(hipMalloc((void **)&sp.games, sizeof(GameEntry) * std::max<int64_t>(games, 1)));
+        sp.games_cap = std::max<int64_t>(games, 1);
+    }
+    sp.game_end = game_end;
+    sp.seed_base = seed_base;
+    sp.temperature = temperature;
+    sp.slots = slots;
+    // every slot starts free; k_finalize hands out games [game_begin, ...)
+    HIP_TRY(hipMemsetAsync(sp.slot, 0, sizeof(Slot) * slots, e->stream));
+    int64_t ctr[4] = {game_begin, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp);
+    if ((rc = check_launch())) return rc;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->selfplay = true;
+    e->sp_arena_used = 0;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_move_begin(uttt_engine_t *e, int32_t *n_live) {
+    if (!e || !e->selfplay) {
+        set_error("uttt_selfplay_move_begin: call uttt_selfplay_begin first");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    const int slots = e->sp.slots;
+    e->tr.n_trees = slots;
+    // roots = the slots' current positions (Slot.state is the first member)
+    std::vector<int32_t> live(slots);
+    HIP_TRY(hipMemcpyAsync(live.data(), e->sp.live, sizeof(int32_t) * slots, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    int nl = 0;
+    for (int v : live) nl += v != 0;
+    if (n_live) *n_live = nl;
+    // gather roots: states are strided inside Slot; copy via a tiny 2D memcpy
+    HIP_TRY(hipMemcpy2DAsync(e->tr.leaf, sizeof(uttt_state_t), e->sp.slot, sizeof(Slot), sizeof(uttt_state_t), slots,
+                             hipMemcpyDeviceToDevice, e->stream));
+    hipLaunchKernelGGL(k_begin, dim3(grid_waves(slots)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+                       (const uttt_state_t *)e->tr.leaf, (const int32_t *)e->sp.live);
+    int rc = check_launch();
+    if (rc) return rc;
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
+    if (!e || !e->selfplay) {
+        set_error("uttt_selfplay_move_end: call uttt_selfplay_begin first");
+        return UTTT_ERR_ORDER;
+    }
+    if (e->phase == 2) {
+        set_error("uttt_selfplay_move_end: pending leaves were not applied");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = check_tree_errors(e);
+    if (rc) return rc;
+    const int slots = e->sp.slots;
+    {
+        TimedLaunch tl(e, kKMoveEnd);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 255) / 256), dim3(256), 0, e->stream, e->pool, e->sp);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
+        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
+    }
+    if ((rc = check_launch())) return rc;
+    int64_t ctr[4];
+    HIP_TRY(hipMemcpyAsync(ctr, e->sp.ctr, sizeof(ctr), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    drain_events(e);
+    if (ctr[2] > e->sp.arena_cap) {
+        set_error("self-play record arena full (%lld plies > %lld)", (long long)ctr[2], (long long)e->sp.arena_cap);
+        return UTTT_ERR_CAPACITY;
+    }
+    e->sp_arena_used = ctr[2];
+    if (n_finished) *n_finished = ctr[1];
+    e->phase = 0;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_games(uttt_engine_t *e, int64_t *game_ids, int64_t *offsets, int32_t *lengths, int64_t max_games,
+                        int64_t *n_games) {
+    if (!e || !e->selfplay) return UTTT_ERR_ORDER;
+    HIP_TRY(hipSetDevice(e->device));
+    int64_t ctr[4];
+    HIP_TRY(hipMemcpyAsync(ctr, e->sp.ctr, sizeof(ctr), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const int64_t n = std::min<int64_t>(ctr[1], e->sp.games_cap);
+    std::vector<GameEntry> g((size_t)n);
+    if (n) HIP_TRY(hipMemcpy(g.data(), e->sp.games, sizeof(GameEntry) * n, hipMemcpyDeviceToHost));
+    std::sort(g.begin(), g.end(), [](const GameEntry &a, const GameEntry &b) { return a.game < b.game; });
+    const int64_t m = std::min<int64_t>(n, max_games);
+    for (int64_t i = 0; i < m; ++i) {
+        if (game_ids) game_ids[i] = g[i].game;
+        if (offsets) offsets[i] = g[i].offset;
+        if (lengths) lengths[i] = (int32_t)g[i].length;
+    }
+    if (n_games) *n_games = n;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_plies(uttt_engine_t *e, uttt_state_t *states, double *policies, int8_t *actions, int8_t *values,
+                        float *inputs_hwc, int64_t max_plies, int64_t *n_plies) {
+    if (!e || !e->selfplay) return UTTT_ERR_ORDER;
+    HIP_TRY(hipSetDevice(e->device));
+    const int64_t n = std::min<int64_t>(e->sp_arena_used, max_plies);
+    if (n_plies) *n_plies = e->sp_arena_used;
+    if (n <= 0) return UTTT_OK;
+    if (states) HIP_TRY(hipMemcpy(states, e->sp.ar_state, sizeof(uttt_state_t) * n, hipMemcpyDeviceToHost));
+    if (policies) HIP_TRY(hipMemcpy(policies, e->sp.ar_policy, sizeof(double) * 81 * n, hipMemcpyDeviceToHost));
+    if (actions) HIP_TRY(hipMemcpy(actions, e->sp.ar_action, n, hipMemcpyDeviceToHost));
+    if (values) HIP_TRY(hipMemcpy(values, e->sp.ar_value, n, hipMemcpyDeviceToHost));
+    if (inputs_hwc) {
+        float *d = nullptr;
+        HIP_TRY(hipMalloc((void **)&d, sizeof(float) * 243 * n));
+        hipLaunchKernelGGL(k_hwc, dim3((unsigned)((n * 81 + 255) / 256)), dim3(256), 0, e->stream, e->sp.ar_state, n, d);
+        hipError_t r = hipGetLastError();
+        if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+        if (r == hipSuccess) r = hipMemcpy(inputs_hwc, d, sizeof(float) * 243 * n, hipMemcpyDeviceToHost);
+        (void)hipFree(d);
+        if (r != hipSuccess) {
+            set_error("history tensor expansion failed: %s", hipGetErrorString(r));
+            return UTTT_ERR_HIP;
+        }
+    }
+    return UTTT_OK;
+}
+
+int uttt_selfplay_get_rng(uttt_engine_t *e, int32_t slot, uint32_t key[624], int32_t *pos) {
+    if (!e || !e->selfplay || slot < 0 || slot >= e->sp.slots || !key || !pos) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpyAsync(key, e->sp.mt_key + (size_t)slot * 624, sizeof(uint32_t) * 624, hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipMemcpyAsync(pos, e->sp.mt_pos + slot, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return UTTT_OK;
+}
+
+int uttt_selfplay_set_rng(uttt_engine_t *e, int32_t slot, const uint32_t key[624], int32_t pos) {
+    if (!e || !e->selfplay || slot < 0 || slot >= e->sp.slots || !key || pos < 0 || pos > 624) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpyAsync(e->sp.mt_key + (size_t)slot * 624, key, sizeof(uint32_t) * 624, hipMemcpyHostToDevice,
+                           e->stream));
+    HIP_TRY(hipMemcpyAsync(e->sp.mt_pos + slot, &pos, sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return UTTT_OK;
+}
+
+// -------------------------------------------------------------- telemetry --
+int uttt_engine_set_timing(uttt_engine_t *e, int32_t enabled) {
+    if (!e) return UTTT_ERR_ARG;
+    e->timing = enabled != 0;
+    return UTTT_OK;
+}
+
+int uttt_engine_kernel_stats(uttt_engine_t *e, int32_t kernel, double *total_ms, int64_t *launches, int64_t *bytes) {
+    if (!e || kernel < 0 || kernel >= kKernelCount) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    drain_events(e);
+    unsigned long long b[kKernelCount];
+    HIP_TRY(hipMemcpy(b, e->d_bytes, sizeof(b), hipMemcpyDeviceToHost));
+    if (total_ms) *total_ms = e->ms[kernel];
+    if (launches) *launches = e->launches[kernel];
+    if (bytes) *bytes = (int64_t)b[kernel];
+    return UTTT_OK;
+}
+
+int uttt_engine_reset_stats(uttt_engine_t *e) {
+    if (!e) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    drain_events(e);
+    for (int k = 0; k < kKernelCount; ++k) {
+        e->ms[k] = 0.0;
+        e->launches[k] = 0;
+    }
+    HIP_TRY(hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return UTTT_OK;
+}
+
+}  // extern "C"

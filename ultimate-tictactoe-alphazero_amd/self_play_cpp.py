@@ -1,0 +1,100 @@
+"""Drop-in for the reference's self_play_cpp.py, on the MI355X engine.
+
+Same names and constants (self_play_cpp.py:26-31), same .history schema
+(:59, :95-99, :125-130). Differences, by design:
+
+* ``self_play()`` plays all SP_GAME_COUNT games concurrently (the reference
+  plays them one after another). Game g draws its moves from
+  ``np.random.RandomState(seed_base + g)``'s stream — equal to the reference's
+  ``play()`` after ``np.random.seed(seed_base + g)``. seed_base defaults to a
+  draw from numpy's global RNG (the reference is unseeded).
+* ``play(model)`` runs one game on the engine and draws from (and advances)
+  numpy's global RNG exactly as the reference does.
+"""
+import os
+import pickle
+import sys
+from datetime import datetime
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+try:
+    import uttt_cpp  # noqa: F401
+    CPP_AVAILABLE = True
+    print("Using C++ backend for MCTS")
+except ImportError:
+    CPP_AVAILABLE = False
+    print("C++ backend not available")
+
+from uttt_amd.model import DualNetwork  # noqa: E402
+from uttt_amd.selfplay import SelfPlay, history_from_records  # noqa: E402
+
+SP_GAME_COUNT = 500
+SP_TEMPERATURE = 1.0
+PV_EVALUATE_COUNT = 50
+MCTS_BATCH_SIZE = 8
+
+device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+_single = {}
+
+
+def _runner(model, slots):
+    key = (id(model), slots)
+    r = _single.get(key)
+    if r is None:
+        _single.clear()
+        r = SelfPlay(slots, PV_EVALUATE_COUNT, MCTS_BATCH_SIZE, SP_TEMPERATURE, model=model)
+        _single[key] = r
+    return r
+
+
+def play(model, use_cpp=True):
+    """One self-play game (self_play_cpp.py:34-101) on numpy's global RNG."""
+    if not (use_cpp and CPP_AVAILABLE):
+        raise RuntimeError("the engine backend is required (build ultimate-tictactoe-alphazero_amd)")
+    model = model.to(device).eval()
+    r = _runner(model, 1)
+    r.begin(0, 1, 0)
+    st = np.random.get_state()
+    r.engine.set_rng(st[1], st[2], slot=0)
+    while r.step():
+        pass
+    key, pos = r.engine.get_rng(0)
+    np.random.set_state((st[0], key, pos, st[3], st[4]))
+    return history_from_records(r.records())
+
+
+def self_play(use_cpp=True, n_games=None, slots=None, seed_base=None, model_path="./model/best.pth",
+              out_dir="./data", model=None):
+    """SP_GAME_COUNT games -> ./data/YYYYmmddHHMMSS.history (self_play_cpp.py:104-130)."""
+    if not (use_cpp and CPP_AVAILABLE):
+        raise RuntimeError("the engine backend is required (build ultimate-tictactoe-alphazero_amd)")
+    n_games = SP_GAME_COUNT if n_games is None else n_games
+    if model is None:
+        model = DualNetwork().to(device)
+        model.load_state_dict(torch.load(model_path, map_location=device, weights_only=True))
+    model = model.to(device).eval()
+    if seed_base is None:
+        seed_base = int(np.random.randint(0, 2**31 - 1))
+    slots = min(n_games, 4096) if slots is None else slots
+    r = SelfPlay(slots, PV_EVALUATE_COUNT, MCTS_BATCH_SIZE, SP_TEMPERATURE, model=model)
+
+    def progress(done, total):
+        print(f"\rSelfPlay {done}/{total} (Backend: HIP)", end="")
+
+    r.run(0, n_games, seed_base, progress)
+    print("")
+    history = history_from_records(r.records())
+    now = datetime.now()
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, "{:04}{:02}{:02}{:02}{:02}{:02}.history".format(
+        now.year, now.month, now.day, now.hour, now.minute, now.second))
+    with open(path, mode="wb") as f:
+        pickle.dump(history, f)
+    return path
+
+
+if __name__ == "__main__":
+    self_play()

@@ -1,0 +1,197 @@
+"""Engine: Python handle on the C ABI (include/uttt_engine.h).
+
+One ``Engine`` owns ``max_trees`` PUCT trees (or self-play slots) in HBM on one
+GPU. All launches go to torch's current stream on that device, so the network
+forward and the tree kernels are ordered without host synchronisation; the only
+per-round sync is reading the number of pending leaves.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import STATE_DTYPE, UtttState, check, ptr
+
+
+def as_states(states):
+    """Sequence of uttt_cpp.State / packed bytes / STATE_DTYPE array -> STATE_DTYPE array."""
+    if isinstance(states, np.ndarray) and states.dtype == STATE_DTYPE:
+        return np.ascontiguousarray(states)
+    out = np.zeros(len(states), STATE_DTYPE)
+    for i, s in enumerate(states):
+        raw = s.packed if hasattr(s, "packed") else bytes(s)
+        out[i:i + 1] = np.frombuffer(raw, STATE_DTYPE)
+    return out
+
+
+def initial_states(n):
+    out = np.zeros(n, STATE_DTYPE)
+    out["active"] = -1
+    return out
+
+
+class Engine:
+    def __init__(self, max_trees, max_sims=50, device=None):
+        import torch
+
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.EngineError("no ROCm GPU visible to torch; the engine runs only on MI355X (gfx950)")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.max_trees = int(max_trees)
+        self.max_sims = int(max_sims)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.lib.uttt_engine_create(self.device, self.max_trees, self.max_sims, ctypes.byref(h)))
+        self.h = h
+        self.n_trees = 0
+        self.n_pending = 0
+        self.use_stream()
+
+    # -------------------------------------------------------------- plumbing --
+    def use_stream(self, stream=None):
+        """Launch on `stream` (default: torch's current stream on this device)."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        check(self.lib.uttt_engine_set_stream(self.h, ctypes.c_void_p(s.cuda_stream)))
+        self.stream = s
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.uttt_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def device_bytes(self):
+        return int(self.lib.uttt_engine_device_bytes(self.h))
+
+    # ---------------------------------------------------------------- search --
+    def search_begin(self, roots, evaluate_count=50, batch_size=8):
+        roots = as_states(roots)
+        check(self.lib.uttt_search_begin(self.h, roots.ctypes.data_as(ctypes.POINTER(UtttState)), len(roots),
+                                         int(evaluate_count), int(batch_size)))
+        self.n_trees = len(roots)
+
+    def select(self, nn_input=None):
+        """One round; writes NCHW inputs into nn_input (device tensor) and returns the pending count."""
+        n = ctypes.c_int32()
+        p = ctypes.c_void_p(nn_input.data_ptr()) if nn_input is not None else None
+        check(self.lib.uttt_search_select(self.h, p, ctypes.byref(n)))
+        self.n_pending = n.value
+        return n.value
+
+    def pending(self):
+        n = self.n_pending
+        st = np.zeros(n, STATE_DTYPE)
+        k = np.zeros(n, np.int32)
+        check(self.lib.uttt_search_pending(self.h, st.ctypes.data_as(ctypes.POINTER(UtttState)), ptr(k, ctypes.c_int32)))
+        return st, k
+
+    def apply(self, policy, value, per_copy=False):
+        """policy: (rows, >=81) f32, value: (rows,) or (rows,1) f32 — device tensors or numpy arrays."""
+        if isinstance(policy, np.ndarray):
+            pol = np.ascontiguousarray(policy, np.float32)
+            val = np.ascontiguousarray(value, np.float32).reshape(-1)
+            check(self.lib.uttt_search_apply(self.h, ctypes.c_void_p(pol.ctypes.data), pol.shape[1],
+                                             ctypes.c_void_p(val.ctypes.data), 1, int(per_copy), 0))
+            return
+        import torch
+
+        assert policy.dtype == torch.float32 and value.dtype == torch.float32
+        assert policy.is_cuda and value.is_cuda
+        if policy.stride(1) != 1:
+            policy = policy.contiguous()
+        vld = value.stride(0)
+        check(self.lib.uttt_search_apply(self.h, ctypes.c_void_p(policy.data_ptr()), policy.stride(0),
+                                         ctypes.c_void_p(value.data_ptr()), vld, int(per_copy), 1))
+
+    def eval_hash(self, nn_input, n, policy, value):
+        check(self.lib.uttt_eval_hash(self.h, ctypes.c_void_p(nn_input.data_ptr()), int(n),
+                                      ctypes.c_void_p(policy.data_ptr()), ctypes.c_void_p(value.data_ptr())))
+
+    def root_visits(self):
+        v = np.zeros((self.n_trees, 81), np.int32)
+        L = np.zeros(self.n_trees, np.int32)
+        check(self.lib.uttt_search_root_visits(self.h, ptr(v, ctypes.c_int32), ptr(L, ctypes.c_int32)))
+        return v, L
+
+    def scores(self, temperature):
+        s = np.zeros((self.n_trees, 81), np.float32)
+        L = np.zeros(self.n_trees, np.int32)
+        check(self.lib.uttt_search_scores(self.h, float(temperature), ptr(s, ctypes.c_float), ptr(L, ctypes.c_int32)))
+        return s, L
+
+    # ------------------------------------------------------------- self-play --
+    def selfplay_begin(self, game_begin, game_end, seed_base, temperature=1.0, evaluate_count=50, batch_size=8,
+                       arena_plies=None):
+        if arena_plies is None:
+            arena_plies = max(81, (game_end - game_begin) * 81)
+        check(self.lib.uttt_selfplay_begin(self.h, int(game_begin), int(game_end), ctypes.c_uint32(seed_base),
+                                           float(temperature), int(evaluate_count), int(batch_size),
+                                           int(arena_plies)))
+        self.n_trees = self.max_trees
+
+    def move_begin(self):
+        n = ctypes.c_int32()
+        check(self.lib.uttt_selfplay_move_begin(self.h, ctypes.byref(n)))
+        return n.value
+
+    def move_end(self):
+        n = ctypes.c_int64()
+        check(self.lib.uttt_selfplay_move_end(self.h, ctypes.byref(n)))
+        return n.value
+
+    def get_rng(self, slot=0):
+        key = np.zeros(624, np.uint32)
+        pos = ctypes.c_int32()
+        check(self.lib.uttt_selfplay_get_rng(self.h, int(slot), ptr(key, ctypes.c_uint32), ctypes.byref(pos)))
+        return key, pos.value
+
+    def set_rng(self, key, pos, slot=0):
+        key = np.ascontiguousarray(key, np.uint32)
+        check(self.lib.uttt_selfplay_set_rng(self.h, int(slot), ptr(key, ctypes.c_uint32), int(pos)))
+
+    def games(self):
+        n = ctypes.c_int64()
+        check(self.lib.uttt_selfplay_games(self.h, None, None, None, 0, ctypes.byref(n)))
+        ids = np.zeros(n.value, np.int64)
+        off = np.zeros(n.value, np.int64)
+        ln = np.zeros(n.value, np.int32)
+        check(self.lib.uttt_selfplay_games(self.h, ptr(ids, ctypes.c_int64), ptr(off, ctypes.c_int64),
+                                           ptr(ln, ctypes.c_int32), n.value, ctypes.byref(n)))
+        return ids, off, ln
+
+    def plies(self, with_inputs=True):
+        n = ctypes.c_int64()
+        check(self.lib.uttt_selfplay_plies(self.h, None, None, None, None, None, 0, ctypes.byref(n)))
+        m = n.value
+        st = np.zeros(m, STATE_DTYPE)
+        pol = np.zeros((m, 81), np.float64)
+        act = np.zeros(m, np.int8)
+        val = np.zeros(m, np.int8)
+        hwc = np.zeros((m, 243), np.float32) if with_inputs else None
+        check(self.lib.uttt_selfplay_plies(
+            self.h, st.ctypes.data_as(ctypes.POINTER(UtttState)), ptr(pol, ctypes.c_double), ptr(act, ctypes.c_int8),
+            ptr(val, ctypes.c_int8), ptr(hwc, ctypes.c_float) if hwc is not None else None, m, ctypes.byref(n)))
+        return {"states": st, "policies": pol, "actions": act, "values": val, "inputs_hwc": hwc}
+
+    # ------------------------------------------------------------- telemetry --
+    def set_timing(self, on=True):
+        check(self.lib.uttt_engine_set_timing(self.h, int(bool(on))))
+
+    def reset_stats(self):
+        check(self.lib.uttt_engine_reset_stats(self.h))
+
+    def kernel_stats(self, name):
+        ms = ctypes.c_double()
+        ln = ctypes.c_int64()
+        by = ctypes.c_int64()
+        check(self.lib.uttt_engine_kernel_stats(self.h, _lib.KERNELS[name], ctypes.byref(ms), ctypes.byref(ln),
+                                                ctypes.byref(by)))
+        return {"ms": ms.value, "launches": ln.value, "bytes": by.value}
