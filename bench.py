@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
     ap.add_argument("--evaluator", choices=["nn", "nn-plain", "hash"], default="nn")
-    ap.add_argument("--cudnn-benchmark", type=int, default=0)
+    ap.add_argument("--age", type=int, default=100,
+                    help="moves played before warmup so the timed population mixes all game phases")
+    ap.add_argument("--cudnn-benchmark", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
@@ -196,9 +198,15 @@ def main():
 
     sp.evaluator = timed_eval
     games_per_rank = 10**9
-    arena = (args.warmup + args.steps + 2) * G
+    arena = (args.age + args.warmup + args.steps + 2) * G
     sp.begin(rank * games_per_rank, (rank + 1) * games_per_rank, 1234, arena_plies=arena)
 
+    # Setup (not warmup, not timed): age the population. All games start together
+    # from the initial position; refilling finished slots with new games spreads
+    # the slots over every phase of a game (openings, middle games with wide
+    # child lists, endgames with terminal simulations) like continuous self-play.
+    for _ in range(args.age):
+        sp.step()
     for _ in range(args.warmup):
         sp.step()
     torch.cuda.synchronize()
@@ -206,7 +214,7 @@ def main():
     nn_stats.update(ms=0.0, rows=0, padded_rows=0)
     sp.engine.reset_stats()
     sp.engine.set_timing(True)
-    rounds0, moves0 = sp.rounds, sp.moves
+    rounds0, finished0 = sp.rounds, sp.finished
 
     if world > 1:
         dist.barrier()
@@ -260,8 +268,9 @@ def main():
                     "random-init DualNetwork (torch.manual_seed(0)); no checkpoint",
             "config": {
                 "workload": f"{G} concurrent self-play games per GPU x {S} sims/move, MCTS_BATCH_SIZE {B}, "
-                            f"tau 1.0 (BASELINE configs[1]/[3] shape; one step = one move of every game)",
-                "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B,
+                            f"tau 1.0, continuous self-play (finished games refilled; population aged "
+                            f"{args.age} moves before warmup); one step = one move of every game",
+                "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
                 "evaluator": {"nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
                               "nn-plain": "DualNetwork 128f x16 fp32 (PyTorch-ROCm/MIOpen)",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],
@@ -289,6 +298,7 @@ def main():
                              "scan": round(scan["ms"], 2), "move_end": round(mend["ms"], 2),
                              "nn": round(nn_stats["ms"], 2), "wall": round(elapsed * 1e3, 2)},
             "rounds_per_step": round(rounds / args.steps, 2),
+            "games_finished_in_timed_steps": int(sp.finished - finished0),
         }
         if not args.no_cpu_baseline:
             cb = run_cpu_baseline(args.cpu_seconds)

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace run of bench.py into profiles/<round>/summary.md.
+
+The bench times only its last `steps` steps; the trace also holds the aging and
+warmup launches. The timed window is recovered as the last `launches` k_select
+dispatches (the bench reports that count), and every kernel is averaged both
+over the whole run and over that window, so the select average can be compared
+with the bench's HIP-event average.
+
+usage: prof_summary.py TRACE.csv BENCH_JSON_LOG OUT.md
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split("(")[0][:80]
+
+
+def main(trace, bench_log, out):
+    with open(bench_log) as f:
+        bench = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+    rows = []
+    with open(trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                         int(r["VGPR_Count"]), int(r["SGPR_Count"]), int(r["Scratch_Size"])))
+    rows.sort()
+    sel = [r for r in rows if "k_select" in r[2]]
+    nwin = bench["roofline"]["launches"]
+    t0 = sel[-nwin][0] if len(sel) >= nwin else rows[0][0]
+    win = [r for r in rows if r[0] >= t0]
+    agg = defaultdict(lambda: [0, 0, 0, 0, 0])
+    for s, e, n, v, sg, sc in win:
+        a = agg[short(n)]
+        a[0] += 1
+        a[1] += e - s
+        a[2], a[3], a[4] = v, sg, sc
+    total = sum(a[1] for a in agg.values())
+    span = win[-1][1] - win[0][0]
+    lines = [f"# rocprofv3 kernel trace — timed window of `{bench_log}`", "",
+             f"bench value (under rocprof): {bench['value']:.0f} sims/s; window = last {nwin} k_select dispatches "
+             f"and everything after; span {span / 1e6:.1f} ms, kernel busy {total / 1e6:.1f} ms", "",
+             "| kernel | calls | total ms | % busy | avg us | VGPR | SGPR | scratch |", "|---|---|---|---|---|---|---|---|"]
+    for n, a in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+        lines.append(f"| `{n}` | {a[0]} | {a[1] / 1e6:.2f} | {100 * a[1] / total:.2f} | {a[1] / a[0] / 1e3:.1f} | "
+                     f"{a[2]} | {a[3]} | {a[4]} |")
+    sw = [r for r in win if "k_select" in r[2]]
+    avg_sel = sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3
+    lines += ["", f"k_select in window: {len(sw)} dispatches, avg {avg_sel:.1f} us (rocprof) vs "
+                  f"{bench['roofline']['avg_launch_us']} us (bench HIP events); "
+                  f"algorithmic bytes/launch {bench['roofline']['algo_bytes_per_launch']} -> "
+                  f"{bench['roofline']['algo_bytes_per_launch'] / (avg_sel * 1e3):.2f} GB/s (rocprof time)"]
+    with open(out, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])

@@ -500,9 +500,13 @@ __device__ void root_scores(const Pool &pool, size_t base, float temperature, fl
         }
         for (int i = 0; i < L; ++i) sc[i] = (i == mi) ? 1.0f : 0.0f;
     } else {
+        // glibc's powf (what the reference's std::pow(float, float) calls) evaluates in
+        // double and rounds once; ocml's f32 powf is not correctly rounded (pow(19, 1)
+        // came out 1 ulp low), so do the same: double pow of the f32 operands, one rounding.
+        const double y = (double)(1.0f / temperature);
         float sum = 0.0f;
         for (int i = 0; i < L; ++i) {
-            sc[i] = powf((float)pool.n[base + first + i], 1.0f / temperature);
+            sc[i] = (float)pow((double)pool.n[base + first + i], y);
             sum += sc[i];
         }
         if (sum > 0)

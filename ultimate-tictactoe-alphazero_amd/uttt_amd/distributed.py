@@ -1,0 +1,110 @@
+"""Multi-GPU self-play: one process per GPU, games sharded by global id.
+
+Game g's result depends only on g (its RandomState(seed_base + g) stream and
+the network), so sharding [0, n) into contiguous blocks per rank and gathering
+the finished records at the end reproduces the single-GPU output exactly for
+any world size. The data path has no collective; the only exchange is the
+optional end-of-cycle gather of compact records to rank 0,
+which rank 0 turns into the reference's .history list (train_network.py:21-24
+reads only the newest file, so it must be one file).
+
+Compact record per ply: packed state (32 B) + policy target (81 f64) +
+action (i8) + value (i8) + game id (i64) = 690 B.
+"""
+import numpy as np
+
+from ._lib import STATE_DTYPE
+
+PLY_DTYPE = np.dtype([("game", "<i8"), ("state", STATE_DTYPE), ("policy", "<f8", (81,)), ("action", "i1"),
+                      ("value", "i1")])
+
+
+def shard(n_games, rank, world):
+    """Contiguous block [begin, end) of game ids for `rank` (sizes differ by at most one)."""
+    base, extra = divmod(int(n_games), int(world))
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def pack_records(records):
+    n = sum(len(r["actions"]) for r in records)
+    out = np.zeros(n, PLY_DTYPE)
+    i = 0
+    for r in records:
+        k = len(r["actions"])
+        out["game"][i:i + k] = r["game"]
+        out["state"][i:i + k] = r["states"]
+        out["policy"][i:i + k] = r["policies"]
+        out["action"][i:i + k] = r["actions"]
+        out["value"][i:i + k] = r["values"]
+        i += k
+    return out
+
+
+def unpack_records(plies):
+    """Inverse of pack_records (plies of one game are contiguous, games sorted by id)."""
+    plies = plies[np.argsort(plies["game"], kind="stable")]
+    games, starts = np.unique(plies["game"], return_index=True)
+    ends = list(starts[1:]) + [len(plies)]
+    recs = []
+    for g, a, b in zip(games.tolist(), starts.tolist(), ends):
+        p = plies[a:b]
+        recs.append({"game": g, "states": p["state"].copy(), "policies": p["policy"].copy(),
+                     "actions": p["action"].astype(np.int64), "values": p["value"].astype(np.int64)})
+    return recs
+
+
+def gather_records(records, dst=0, group=None):
+    """Gather every rank's finished games to `dst` (torch.distributed, any backend).
+    Returns the merged records sorted by game id on dst, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    local = pack_records(records).view(np.uint8)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    backend = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    n = torch.tensor([local.size], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    cap = max(sizes) if sizes else 0
+    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    if local.size:
+        buf[:local.size] = torch.from_numpy(local).to(dev)
+    bufs = [torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)  # one fixed-size exchange (nccl has no variable gather)
+    if rank != dst:
+        return None
+    parts = [b[:s].cpu().numpy().view(PLY_DTYPE) for b, s in zip(bufs, sizes)]
+    return unpack_records(np.concatenate(parts) if parts else np.zeros(0, PLY_DTYPE))
+
+
+def records_to_inputs(records):
+    """Add the (9,9,3) input tensors (uttt_game.cpp:244-280) from the packed states, on the host rules."""
+    import ctypes
+
+    from . import _lib
+    lib = _lib.load()
+    for r in records:
+        st = np.ascontiguousarray(r["states"])
+        x = np.zeros((len(st), 243), np.float32)
+        for i in range(len(st)):
+            lib.uttt_state_input_hwc(st[i:i + 1].ctypes.data_as(ctypes.POINTER(_lib.UtttState)),
+                                     x[i].ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        r["inputs"] = x.reshape(len(st), 9, 9, 3)
+    return records
+
+
+def self_play_sharded(model, n_games, slots, seed_base, evaluate_count=50, batch_size=8, temperature=1.0):
+    """Run this rank's shard of [0, n_games) and gather to rank 0 (returns records on rank 0)."""
+    import torch.distributed as dist
+
+    from .selfplay import SelfPlay
+    rank, world = dist.get_rank(), dist.get_world_size()
+    b, e = shard(n_games, rank, world)
+    sp = SelfPlay(max(1, min(slots, e - b)), evaluate_count, batch_size, temperature, model=model)
+    sp.run(b, e, seed_base)
+    recs = gather_records(sp.records(with_inputs=False))
+    return records_to_inputs(recs) if recs is not None else None

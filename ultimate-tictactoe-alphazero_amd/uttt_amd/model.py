@@ -110,6 +110,11 @@ class FoldedDualNetwork(nn.Module):
 
     @torch.no_grad()
     def forward(self, x):
+        logits, v = self.forward_logits(x)
+        return F.softmax(logits, dim=1), v
+
+    @torch.no_grad()
+    def forward_logits(self, x):
         x = x.contiguous(memory_format=torch.channels_last)
         x = F.relu(F.conv2d(x, self.stem[0], self.stem[1], padding=1))
         for (w1, b1), (w2, b2) in self.blocks:
@@ -117,11 +122,25 @@ class FoldedDualNetwork(nn.Module):
             x = F.relu(F.conv2d(y, w2, b2, padding=1) + x)
         p = F.relu(F.conv2d(x, self.pconv[0], self.pconv[1]))
         p = torch.flatten(p.contiguous(), 1)
-        p = F.softmax(F.linear(p, *self.pfc), dim=1)
+        logits = F.linear(p, *self.pfc)
         v = F.relu(F.conv2d(x, self.vconv[0], self.vconv[1]))
         v = torch.flatten(v.contiguous(), 1)
         v = torch.tanh(F.linear(F.relu(F.linear(v, *self.vfc1)), *self.vfc2))
-        return p, v
+        return logits, v
+
+
+def policy_logits(net, x):
+    """(pre-softmax policy logits, value) of a DualNetwork (hook on policy_fc)."""
+    if hasattr(net, "forward_logits"):
+        return net.forward_logits(x)
+    box = {}
+    h = net.policy_fc.register_forward_hook(lambda m, i, o: box.setdefault("z", o))
+    try:
+        with torch.no_grad():
+            _, v = net(x)
+    finally:
+        h.remove()
+    return box["z"], v
 
 
 def random_network(seed=0, device="cpu"):

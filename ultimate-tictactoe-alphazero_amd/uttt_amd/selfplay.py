@@ -14,7 +14,7 @@ import torch
 from .engine import Engine, initial_states
 
 
-def _bucket(n, cap, quantum=128):
+def _bucket(n, cap, quantum=256):
     """Round a batch up so the network sees few distinct shapes (MIOpen tuning)."""
     if n <= 64:
         b = 1 << max(0, math.ceil(math.log2(max(n, 1))))
