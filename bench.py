@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["nn", "nn-plain", "hash"], default="nn")
+    ap.add_argument("--evaluator", choices=["fused", "nn", "nn-plain", "hash"], default="fused")
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
     ap.add_argument("--cudnn-benchmark", type=int, default=1)
@@ -159,6 +159,7 @@ def main():
     sys.path.insert(0, PKG)
     from uttt_amd import HashEvaluator, NetworkEvaluator, SelfPlay
     from uttt_amd.model import FoldedDualNetwork, random_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -177,6 +178,8 @@ def main():
     sp = SelfPlay(G, S, B, 1.0, device=local, model=model)
     if args.evaluator == "hash":
         sp.evaluator = HashEvaluator(sp.engine)
+    elif args.evaluator == "fused":
+        sp.evaluator = FusedNetworkEvaluator(net, sp.engine)
 
     # NN timing (events on the stream the evaluator runs on) and useful rows
     nn_stats = {"ms": 0.0, "rows": 0, "padded_rows": 0}
@@ -191,11 +194,12 @@ def main():
         b.record()
         ev_pairs.append((a, b))
         nn_stats["rows"] += n
-        if isinstance(inner, NetworkEvaluator):
+        if isinstance(inner, (NetworkEvaluator, FusedNetworkEvaluator)):
             from uttt_amd.selfplay import _bucket
             nn_stats["padded_rows"] += _bucket(n, G)
         return out
 
+    timed_eval.needs_input = getattr(inner, "needs_input", True)
     sp.evaluator = timed_eval
     games_per_rank = 10**9
     arena = (args.age + args.warmup + args.steps + 2) * G
@@ -271,7 +275,9 @@ def main():
                             f"tau 1.0, continuous self-play (finished games refilled; population aged "
                             f"{args.age} moves before warmup); one step = one move of every game",
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
-                "evaluator": {"nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
+                "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; 3x3 convs MIOpen NHWC, stem/"
+                                       "epilogues/heads as HIP kernels (csrc/nn_kernels.hip)",
+                              "nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
                               "nn-plain": "DualNetwork 128f x16 fp32 (PyTorch-ROCm/MIOpen)",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],
                 "parallelism": f"games sharded over {world} GPU(s), no data-path collective",

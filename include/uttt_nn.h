@@ -1,0 +1,52 @@
+/*
+ * uttt_nn.h — C ABI of the DualNetwork leaf-evaluator kernels (dual_network.py:89-121,
+ * inference form: BatchNorm folded into each convolution, activations NHWC f32,
+ * 128 channels). The 3x3 128->128 convolutions themselves are computed by the
+ * caller (MIOpen through PyTorch-ROCm); these kernels replace everything else.
+ */
+#ifndef UTTT_NN_H
+#define UTTT_NN_H
+
+#include <stdint.h>
+
+#include "uttt_engine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Layout of the packed head-weight block (floats), all BN-folded:
+ *   policy 1x1 conv W[2][128], b[2]; value 1x1 conv W[128], b[1];
+ *   policy FC W[81][162] (input index = plane*81 + position, torch.flatten of NCHW), b[81];
+ *   value FC1 W[256][81], b[256]; value FC2 W[256], b[1]. */
+#define UTTT_HEAD_PCONV_W 0
+#define UTTT_HEAD_PCONV_B (UTTT_HEAD_PCONV_W + 2 * 128)
+#define UTTT_HEAD_VCONV_W (UTTT_HEAD_PCONV_B + 2)
+#define UTTT_HEAD_VCONV_B (UTTT_HEAD_VCONV_W + 128)
+#define UTTT_HEAD_PFC_W (UTTT_HEAD_VCONV_B + 1)
+#define UTTT_HEAD_PFC_B (UTTT_HEAD_PFC_W + 81 * 162)
+#define UTTT_HEAD_VFC1_W (UTTT_HEAD_PFC_B + 81)
+#define UTTT_HEAD_VFC1_B (UTTT_HEAD_VFC1_W + 256 * 81)
+#define UTTT_HEAD_VFC2_W (UTTT_HEAD_VFC1_B + 256)
+#define UTTT_HEAD_VFC2_B (UTTT_HEAD_VFC2_W + 256)
+#define UTTT_HEAD_SIZE (UTTT_HEAD_VFC2_B + 1)
+
+/* Stem from the engine's pending leaves (slot order, after uttt_search_select):
+ * out[n][81][128] = relu(conv3x3(planes, w) + b) with w[27][128] = folded
+ * conv_input weight laid out [in_plane*9 + ky*3 + kx][out_channel]
+ * (dual_network.py:89-92; planes of uttt_game.cpp:244-280). Engine stream. */
+int uttt_nn_stem(uttt_engine_t *eng, const float *w, const float *b, float *out);
+/* y = relu(x + bias[c] (+ residual)) over rows x channels (NHWC); residual may be NULL
+ * (ResidualBlock, dual_network.py:36-45, minus the convolutions). */
+int uttt_nn_epilogue(const float *x, const float *bias, const float *residual, float *y, int64_t rows,
+                     int32_t channels, void *stream);
+/* Policy softmax (n,81) (logits if softmax == 0) and tanh value (n) from the final
+ * activation (n,81,128) (dual_network.py:106-121). */
+int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float *policy, float *value,
+                  int32_t softmax, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UTTT_NN_H */

@@ -279,3 +279,55 @@ def test_full_size_4096x50_properties_and_samples(gpu, oracle_lib):
         for i in range(0, 4096, 97):
             _, vi, _ = core.pv_mcts_scores_hash(ostates[i], 1.0, S, B)
             assert np.array_equal(visits[i, :L[i]], vi), (S, B, i)
+
+
+def test_fused_evaluator_matches_cpu_fp32(gpu, oracle_lib):
+    """Stem-from-bitboards + MIOpen NHWC convs + HIP epilogues + HIP heads vs the
+    plain DualNetwork on CPU fp32, on real pending leaves of a search."""
+    import torch
+    from uttt_amd.model import policy_logits, random_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    roots, _ = _random_positions(oracle_lib, 300, seed=13)
+    net = random_network(0, "cuda")
+    bs = gpu.BatchedSearch(len(roots), 50)
+    fused = FusedNetworkEvaluator(net, bs.engine)
+    cpu = random_network(0)
+    e = bs.engine
+    e.use_stream()
+    e.search_begin(roots, 50, 8)
+    for _ in range(3):  # a few rounds: leaves at depth 1 and 2
+        n = e.select(bs.x)
+        z, v = fused.forward(n, softmax=False)
+        z_cpu, v_cpu = policy_logits(cpu, bs.x[:n].cpu())
+        assert (v.cpu() - v_cpu.reshape(-1)).abs().max().item() <= 1e-5
+        scale = z_cpu.abs().amax(dim=1, keepdim=True).clamp_min(1.0)
+        assert ((z.cpu() - z_cpu).abs() / scale).max().item() <= 1e-4
+        p, v2 = fused.forward(n, softmax=True)
+        assert torch.allclose(p.sum(dim=1).cpu(), torch.ones(n), atol=1e-5)
+        e.apply(p, v2)
+
+
+def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib):
+    """Search with the fused evaluator; its outputs replayed into the oracle give
+    the same root visit counts."""
+    from uttt_amd.model import random_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 48, seed=17)
+    bs = gpu.BatchedSearch(len(roots), 50)
+    fused = FusedNetworkEvaluator(random_network(0, "cuda"), bs.engine)
+    table = {}
+
+    def recording(x, n):
+        p, v = fused(x, n)
+        xs = x[:n].cpu().numpy().reshape(n, 243)
+        ps, vs = p.cpu().numpy(), v.cpu().numpy().reshape(-1)
+        for i in range(n):
+            table[xs[i].tobytes()] = (ps[i].copy(), np.float32(vs[i]))
+        return p, v
+
+    bs.run(roots, recording, 50, 8)  # plain function: needs_input -> select writes x
+    visits, L = bs.visits()
+    for i, s in enumerate(ostates):
+        _, vi, _ = core.pv_mcts_scores(s, 1.0, 50, 8, lambda x: table[np.asarray(x, np.float32).tobytes()])
+        assert np.array_equal(visits[i, :L[i]], vi), i

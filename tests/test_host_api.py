@@ -13,8 +13,10 @@ from conftest import GOLDEN, REPO, golden
 
 
 def _declared_functions():
-    with open(os.path.join(REPO, "include", "uttt_engine.h")) as f:
-        src = f.read()
+    src = ""
+    for h in ("uttt_engine.h", "uttt_nn.h"):
+        with open(os.path.join(REPO, "include", h)) as f:
+            src += f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w]+\s*\*?\s*(uttt_\w+)\s*\(", src, flags=re.M)))
 

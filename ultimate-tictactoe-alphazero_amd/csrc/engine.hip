@@ -939,6 +939,23 @@ int ensure_scratch(uttt_engine *e, int64_t rows) {
 
 }  // namespace
 
+namespace uttt {
+// For the evaluator kernels (nn_kernels.hip): the pending leaves of the current round.
+int engine_pending_view(uttt_engine_t *e, const uttt_state_t **leaf, const int32_t **tree_of, int32_t *n,
+                        hipStream_t *stream) {
+    if (!e) return UTTT_ERR_ARG;
+    if (e->phase != 2) {
+        set_error("no pending leaves (call uttt_search_select first)");
+        return UTTT_ERR_ORDER;
+    }
+    *leaf = e->tr.leaf;
+    *tree_of = e->tr.tree_of;
+    *n = e->n_pending;
+    *stream = e->stream;
+    return UTTT_OK;
+}
+}  // namespace uttt
+
 extern "C" {
 
 const char *uttt_last_error(void) { return g_err.c_str(); }

@@ -1,0 +1,107 @@
+"""FusedNetworkEvaluator: the DualNetwork leaf evaluator with its non-GEMM parts
+as gfx950 kernels (csrc/nn_kernels.hip, include/uttt_nn.h):
+
+  leaves --k_stem--> act (n,9,9,128 NHWC, relu(conv_input+bn) applied)
+  16 x [ MIOpen conv3x3 (NHWC, no bias) -> k_epilogue(relu(. + b1))
+         MIOpen conv3x3 -> k_epilogue(relu(. + b2 + residual)) ]
+  --k_heads--> policy (n,81) softmax, value (n,)
+
+Replaces, per forward, the engine's NCHW encode, MIOpen's stem conv (naive /
+ck grouped kernels for 3 input channels), every separate bias / ReLU / add
+pass, and the head convs + FCs. BatchNorm is folded (eval mode), so the
+function is the reference's dual_network.py:89-121 up to fp32 rounding order.
+"""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import check
+from .model import fold_bn
+from .selfplay import _bucket
+
+HEAD = {}
+
+
+def _head_layout():
+    if not HEAD:
+        o = 0
+        for name, size in (("pconv_w", 2 * 128), ("pconv_b", 2), ("vconv_w", 128), ("vconv_b", 1),
+                           ("pfc_w", 81 * 162), ("pfc_b", 81), ("vfc1_w", 256 * 81), ("vfc1_b", 256),
+                           ("vfc2_w", 256), ("vfc2_b", 1)):
+            HEAD[name] = (o, size)
+            o += size
+        HEAD["size"] = o
+    return HEAD
+
+
+def pack_heads(net, device):
+    lay = _head_layout()
+    buf = torch.zeros(lay["size"], dtype=torch.float32)
+    pw, pb = fold_bn(net.policy_conv, net.policy_bn)
+    vw, vb = fold_bn(net.value_conv, net.value_bn)
+    parts = {"pconv_w": pw.reshape(-1), "pconv_b": pb, "vconv_w": vw.reshape(-1), "vconv_b": vb,
+             "pfc_w": net.policy_fc.weight.reshape(-1), "pfc_b": net.policy_fc.bias,
+             "vfc1_w": net.value_fc1.weight.reshape(-1), "vfc1_b": net.value_fc1.bias,
+             "vfc2_w": net.value_fc2.weight.reshape(-1), "vfc2_b": net.value_fc2.bias}
+    for k, v in parts.items():
+        o, n = lay[k]
+        assert v.numel() == n, (k, v.numel(), n)
+        buf[o:o + n] = v.detach().float().cpu()
+    return buf.to(device)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class FusedNetworkEvaluator:
+    needs_input = False
+
+    def __init__(self, net, engine, max_batch=None):
+        net = net.eval()
+        self.engine = engine
+        self.lib = _lib.load()
+        dev = torch.device("cuda", engine.device)
+        self.max_batch = max_batch or engine.max_trees
+        with torch.no_grad():
+            sw, sb = fold_bn(net.conv_input, net.bn_input)            # (128,3,3,3)
+            self.stem_w = sw.permute(1, 2, 3, 0).reshape(27, 128).contiguous().to(dev)
+            self.stem_b = sb.contiguous().to(dev)
+            cl = torch.channels_last
+            self.blocks = []
+            for b in net.residual_blocks:
+                w1, b1 = fold_bn(b.conv1, b.bn1)
+                w2, b2 = fold_bn(b.conv2, b.bn2)
+                self.blocks.append((w1.to(dev).contiguous(memory_format=cl), b1.to(dev),
+                                    w2.to(dev).contiguous(memory_format=cl), b2.to(dev)))
+            self.heads = pack_heads(net, dev)
+        self.act = torch.zeros((self.max_batch, 9, 9, 128), dtype=torch.float32, device=dev)
+        self.policy = torch.zeros((self.max_batch, 81), dtype=torch.float32, device=dev)
+        self.value = torch.zeros((self.max_batch,), dtype=torch.float32, device=dev)
+
+    def _epilogue(self, x, bias, res, out, stream):
+        check(self.lib.uttt_nn_epilogue(_p(x), _p(bias), _p(res) if res is not None else None, _p(out),
+                                        x.numel() // 128, 128, ctypes.c_void_p(stream)))
+
+    @torch.no_grad()
+    def forward(self, n, softmax=True):
+        """Evaluate the engine's n pending leaves; returns (policy or logits (n,81), value (n,))."""
+        stream = torch.cuda.current_stream(self.engine.device).cuda_stream
+        nb = _bucket(n, self.max_batch)
+        check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(self.act)))
+        a = self.act[:nb].permute(0, 3, 1, 2)  # NCHW view, channels-last strides
+        for w1, b1, w2, b2 in self.blocks:
+            y = F.conv2d(a, w1, None, padding=1)
+            assert y.is_contiguous(memory_format=torch.channels_last)
+            self._epilogue(y, b1, None, y, stream)
+            z = F.conv2d(y, w2, None, padding=1)
+            self._epilogue(z, b2, a, z, stream)
+            a = z
+        check(self.lib.uttt_nn_heads(_p(a), _p(self.heads), n, _p(self.policy), _p(self.value),
+                                     1 if softmax else 0, ctypes.c_void_p(stream)))
+        return self.policy[:n], self.value[:n]
+
+    def __call__(self, x, n):
+        return self.forward(n, True)

@@ -65,8 +65,9 @@ class BatchedSearch:
         e.use_stream()
         e.search_begin(roots, evaluate_count, batch_size)
         self.rounds = 0
+        x = self.x if getattr(evaluator, "needs_input", True) else None
         while True:
-            n = e.select(self.x)
+            n = e.select(x)
             if n == 0:
                 break
             p, v = evaluator(self.x, n)
@@ -117,8 +118,9 @@ class SelfPlay:
         live = e.move_begin()
         if live == 0:
             return 0
+        x = self.x if getattr(self.evaluator, "needs_input", True) else None
         while True:
-            n = e.select(self.x)
+            n = e.select(x)
             if n == 0:
                 break
             p, v = self.evaluator(self.x, n)
