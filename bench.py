@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
     ap.add_argument("--cudnn-benchmark", type=int, default=1)
+    ap.add_argument("--cache-log2", type=int, default=21, help="evaluation cache entries (log2); 0 = off")
+    ap.add_argument("--tag", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
@@ -175,7 +177,7 @@ def main():
     G, S, B = args.games, args.sims, args.batch
     net = random_network(0, dev)
     model = FoldedDualNetwork(net).to(dev) if args.evaluator == "nn" else net
-    sp = SelfPlay(G, S, B, 1.0, device=local, model=model)
+    sp = SelfPlay(G, S, B, 1.0, device=local, model=model, cache_log2=args.cache_log2)
     if args.evaluator == "hash":
         sp.evaluator = HashEvaluator(sp.engine)
     elif args.evaluator == "fused":
@@ -240,6 +242,7 @@ def main():
     scan = sp.engine.kernel_stats("scan")
     mend = sp.engine.kernel_stats("move_end")
     rounds = sp.rounds - rounds0
+    cache = sp.engine.cache_stats() if args.cache_log2 else None
 
     tot = torch.tensor([float(sims), elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -275,6 +278,7 @@ def main():
                             f"tau 1.0, continuous self-play (finished games refilled; population aged "
                             f"{args.age} moves before warmup); one step = one move of every game",
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
+                "eval_cache_log2": args.cache_log2,
                 "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; 3x3 convs MIOpen NHWC, stem/"
                                        "epilogues/heads as HIP kernels (csrc/nn_kernels.hip)",
                               "nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
@@ -305,6 +309,8 @@ def main():
                              "nn": round(nn_stats["ms"], 2), "wall": round(elapsed * 1e3, 2)},
             "rounds_per_step": round(rounds / args.steps, 2),
             "games_finished_in_timed_steps": int(sp.finished - finished0),
+            "eval_cache": (dict(cache, hit_rate=round(cache["hits"] / max(cache["hits"] + cache["misses"], 1), 4),
+                                log2_capacity=args.cache_log2) if cache else None),
         }
         if not args.no_cpu_baseline:
             cb = run_cpu_baseline(args.cpu_seconds)

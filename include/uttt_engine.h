@@ -166,6 +166,18 @@ int uttt_selfplay_games(uttt_engine_t *eng, int64_t *game_ids, int64_t *offsets,
 int uttt_selfplay_plies(uttt_engine_t *eng, uttt_state_t *states, double *policies, int8_t *actions,
                         int8_t *values, float *inputs_hwc, int64_t max_plies, int64_t *n_plies);
 
+/* ----------------------------------------------------- evaluation cache --- */
+/* Position -> raw evaluator output table in HBM (2^log2_capacity entries of
+ * 360 B; 0 = off, the default). A flushed leaf whose position is cached is
+ * expanded from the table inside the select kernel instead of waiting for the
+ * evaluator. Exact for a deterministic evaluator (the evaluator sees only the
+ * position, uttt_game.cpp:244-280). Self-play clears it at begin and every
+ * clear_every_moves moves (0 = never); per-copy apply bypasses it. */
+int uttt_engine_set_cache(uttt_engine_t *eng, int32_t log2_capacity, int32_t clear_every_moves);
+int uttt_engine_cache_clear(uttt_engine_t *eng);
+/* hits: leaves resolved from the table; misses: leaves sent to the evaluator. */
+int uttt_engine_cache_stats(uttt_engine_t *eng, int64_t *hits, int64_t *misses, int64_t *inserts);
+
 /* ------------------------------------------------------------ telemetry --- */
 /* Per-kernel timing with HIP events on the engine's stream (off by default). */
 int uttt_engine_set_timing(uttt_engine_t *eng, int32_t enabled);

@@ -331,3 +331,20 @@ def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib):
     for i, s in enumerate(ostates):
         _, vi, _ = core.pv_mcts_scores(s, 1.0, 50, 8, lambda x: table[np.asarray(x, np.float32).tobytes()])
         assert np.array_equal(visits[i, :L[i]], vi), i
+
+
+def test_eval_cache_is_exact(gpu, oracle_lib):
+    """With the evaluation cache on, repeated and overlapping searches resolve
+    leaves from the table and still match the oracle bit for bit."""
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 256, seed=23)
+    bs = gpu.BatchedSearch(len(roots), 400, cache_log2=16)
+    ev = gpu.HashEvaluator(bs.engine)
+    for rep, (S, B) in enumerate([(50, 8), (50, 8), (120, 4), (50, 1)]):
+        bs.run(roots, ev, S, B)
+        visits, L = bs.visits()
+        for i in range(0, len(ostates), 5):
+            _, vi, _ = core.pv_mcts_scores_hash(ostates[i], 1.0, S, B)
+            assert np.array_equal(visits[i, :L[i]], vi), (rep, S, B, i)
+    st = bs.engine.cache_stats()
+    assert st["hits"] > 0 and st["inserts"] > 0

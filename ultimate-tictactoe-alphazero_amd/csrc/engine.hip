@@ -146,6 +146,154 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 // read what one lane wrote; same CU, so workgroup scope suffices).
 __device__ __forceinline__ void wave_memory_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
+// ------------------------------------------------------ evaluation cache --
+// Open-addressing table in HBM: position (32 B) -> raw evaluator output (81
+// priors + value, before legal masking). The evaluator is a pure function of
+// the position (the reference feeds it to_input_tensor(), uttt_game.cpp:244),
+// so a hit replays exactly what a new evaluation would return. Looked up in
+// k_select (a hit is expanded in place: no network round), filled by k_apply.
+constexpr int kProbe = 8;
+constexpr int kCacheVal = 82;
+
+struct EvalCache {
+    uint32_t *flag;      // 0 empty, 1 claimed, 2 ready
+    uttt_state_t *key;
+    float *val;          // [slot][82]
+    uint32_t mask;       // capacity - 1
+    unsigned long long *ctr;  // [0] hits, [1] misses (network leaves), [2] inserts
+};
+
+__device__ __forceinline__ uint32_t state_hash(const uttt_state_t &s) {
+    const uint64_t a = ((uint64_t)s.own[1] << 32) | s.own[0];
+    const uint64_t b = ((uint64_t)s.opp[0] << 32) | s.own[2];
+    const uint64_t c = ((uint64_t)s.opp[2] << 32) | s.opp[1];
+    const uint64_t d = ((uint64_t)(uint32_t)s.active << 32) | s.mains;
+    return (uint32_t)mix64(mix64(mix64(mix64(kGold ^ a) ^ b) ^ c) ^ d);
+}
+
+__device__ __forceinline__ bool same_state(const uttt_state_t &x, const uttt_state_t &y) {
+    return x.own[0] == y.own[0] && x.own[1] == y.own[1] && x.own[2] == y.own[2] && x.opp[0] == y.opp[0] &&
+           x.opp[1] == y.opp[1] && x.opp[2] == y.opp[2] && x.mains == y.mains && x.active == y.active;
+}
+
+// Wave-uniform lookup, the kProbe slots probed by lanes 0..kProbe-1 at once:
+// a hit counts only if no empty slot precedes it in probe order.
+__device__ __forceinline__ int cache_find(const EvalCache &c, const uttt_state_t &s) {
+    if (!c.flag) return -1;
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t slot = (state_hash(s) + (uint32_t)lane) & c.mask;
+    uint32_t f = 0u;
+    bool same = false;
+    if (lane < kProbe) {
+        f = c.flag[slot];
+        if (f == 2u) same = same_state(c.key[slot], s);
+    }
+    const uint64_t hit = __ballot(lane < kProbe && f == 2u && same);
+    const uint64_t empty = __ballot(lane < kProbe && f == 0u);
+    if (!hit) return -1;
+    const int hl = __builtin_ctzll(hit);
+    if (empty && __builtin_ctzll(empty) < hl) return -1;
+    return __builtin_amdgcn_readfirstlane((int)((state_hash(s) + (uint32_t)hl) & c.mask));
+}
+
+// Wave-level insert of (s -> pol[0..80], v). Lane 0 claims a slot by CAS;
+// a concurrent insert of the same key may leave a harmless duplicate.
+__device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const float *pol, float v) {
+    if (!c.flag) return;
+    const int lane = (int)(threadIdx.x & 63);
+    int slot = -1;
+    if (lane == 0) {
+        const uint32_t h = state_hash(s);
+        for (int i = 0; i < kProbe; ++i) {
+            const uint32_t sl = (h + (uint32_t)i) & c.mask;
+            const uint32_t f = __hip_atomic_load(c.flag + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f == 2u && same_state(c.key[sl], s)) break;
+            if (f == 0u && atomicCAS(c.flag + sl, 0u, 1u) == 0u) {
+                slot = (int)sl;
+                break;
+            }
+        }
+    }
+    slot = __shfl(slot, 0);
+    if (slot < 0) return;
+    float *dst = c.val + (size_t)slot * kCacheVal;
+    dst[lane] = pol[lane];
+    if (lane < 17) dst[64 + lane] = pol[64 + lane];
+    if (lane == 17) dst[81] = v;
+    if (lane == 0) c.key[slot] = s;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) {
+        __hip_atomic_store(c.flag + slot, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(c.ctr + 2, 1ull);
+    }
+}
+
+// ---------------------------------------------------------- expand + backup --
+// uttt_mcts.cpp:138-167 for k identical copies of one flushed leaf: priors =
+// pol[a] for legal a, sequential f32 sum in action order, divide (uniform
+// 1/|legal| if the sum is <= 0); append k child blocks (expand never clears,
+// :38-43); back up v k times along path[0..depth] (:47-54, leaf first, sign
+// flipping upward). Lane d holds path[d] in path_lo and path[64+d] in path_hi.
+// Returns false without writing when the node pool would overflow.
+__device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi, int k,
+                              const uttt_state_t &s, const float *pol, float v, int &node_count) {
+    const int lane = lane_id();
+    uint32_t m[3];
+    legal_mask(s, m);
+    const bool l0 = bit_of(m, lane) != 0u;
+    const bool l1 = lane < 17 && bit_of(m, 64 + lane) != 0u;
+    const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
+    const int L = __popcll(b0) + __popcll(b1);
+    const int nb = node_count;
+    if ((int64_t)nb + (int64_t)k * L > pool.cap || L == 0) return false;
+    const int i0 = __popcll(b0 & lanes_below());
+    const int i1 = __popcll(b0) + __popcll(b1 & lanes_below());
+    const float p0 = l0 ? pol[lane] : 0.0f;
+    const float p1 = l1 ? pol[64 + lane] : 0.0f;
+    float sum = 0.0f;
+    for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
+    for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+    const float un = 1.0f / (float)L;
+    const float q0 = sum > 0 ? p0 / sum : un;
+    const float q1 = sum > 0 ? p1 / sum : un;
+    for (int j = 0; j < k; ++j) {
+        const size_t blk = base + nb + (size_t)j * L;
+        if (l0) {
+            pool.n[blk + i0] = 0;
+            pool.w[blk + i0] = 0.0f;
+            pool.p[blk + i0] = q0;
+            pool.link[blk + i0] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
+        }
+        if (l1) {
+            pool.n[blk + i1] = 0;
+            pool.w[blk + i1] = 0.0f;
+            pool.p[blk + i1] = q1;
+            pool.link[blk + i1] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
+        }
+    }
+    if (lane <= depth) {
+        float w = pool.w[base + path_lo];
+        const float x = ((depth - lane) & 1) ? -v : v;
+        for (int j = 0; j < k; ++j) w += x;
+        pool.w[base + path_lo] = w;
+        pool.n[base + path_lo] += k;
+    }
+    if (lane + 64 <= depth) {
+        float w = pool.w[base + path_hi];
+        const float x = ((depth - lane - 64) & 1) ? -v : v;
+        for (int j = 0; j < k; ++j) w += x;
+        pool.w[base + path_hi] = w;
+        pool.n[base + path_hi] += k;
+    }
+    if (lane == 0) {
+        const uint2 old = pool.link[base + node];
+        pool.link[base + node] =
+            make_uint2((uint32_t)nb, pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y)));
+    }
+    node_count = nb + k * L;
+    return true;
+}
+
 // ----------------------------------------------------------- root (begin) --
 // uttt_mcts.cpp:92-103: root expanded at once with uniform priors 1.0f/|legal|.
 // Self-play passes `live` (slot flags); search passes nullptr (all live).
@@ -198,7 +346,8 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 // Terminal simulations are backed up in place (:115-118). The k-1 further
 // simulations the reference spends re-finding the same queued leaf are
 // accounted by k.
-__global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, unsigned long long *bytes_ctr) {
+__global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCache cache,
+                                                   unsigned long long *bytes_ctr) {
     const int lane = lane_id();
     const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (t >= tr.n_trees) return;
@@ -288,6 +437,21 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, unsigned
             // Unexpanded leaf (n == 0 && no children, uttt_mcts.cpp:121): queue it with
             // k = the copies the reference would queue before flushing (:127).
             const int k = min(tr.batch, tr.sims - sims_done);
+            const int hit = cache_find(cache, s);
+            if (hit >= 0) {  // the flush's evaluation is already known: apply it now
+                const float *cv = cache.val + (size_t)hit * kCacheVal;
+                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count)) {
+                    if (lane == 0) ctl.status |= kErrCapacity;
+                    break;
+                }
+                wave_memory_fence();
+                if (lane == 0) atomicAdd(cache.ctr, 1ull);
+                bytes += 20ull * (unsigned long long)(k * meta_L(LK[node].y)) + 16ull * (depth + 1);
+                sims_done += k;
+                if (sims_done >= tr.sims) break;
+                continue;
+            }
+            if (cache.flag && lane == 0) atomicAdd(cache.ctr + 1, 1ull);
             int32_t *gp = tr.path + (size_t)t * kMaxDepth;
             if (lane <= depth) gp[lane] = path_lo;
             if (lane + 64 <= depth) gp[lane + 64] = path_hi;
@@ -361,7 +525,7 @@ __global__ __launch_bounds__(256) void k_encode(Trees tr, float *__restrict__ x,
 // legal priors, sequential f32 sum in action order, divide (uniform 1/|legal|
 // if sum <= 0), append the child block, back up the value along the path.
 // per_copy: row rowbase[slot] + j holds copy j's result; else row = slot.
-__global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, const float *__restrict__ policy,
+__global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache cache, const float *__restrict__ policy,
                                                   int64_t pld, const float *__restrict__ value, int64_t vld,
                                                   const int32_t *__restrict__ rowbase, int per_copy,
                                                   unsigned long long *bytes_ctr) {
@@ -373,81 +537,93 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, const flo
     TreeCtl ctl = tr.ctl[t];
     const uttt_state_t s = tr.leaf[t];
     const size_t base = (size_t)t * pool.cap;
-    uint32_t m[3];
-    legal_mask(s, m);
-    const bool l0 = bit_of(m, lane) != 0u;
-    const bool l1 = lane < 17 && bit_of(m, 64 + lane) != 0u;
-    const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
-    const int L = __popcll(b0) + __popcll(b1);
-    const int i0 = __popcll(b0 & lanes_below());
-    const int i1 = __popcll(b0) + __popcll(b1 & lanes_below());
-    const int k = r.k;
-    const int nb = ctl.node_count;
-    if ((int64_t)nb + (int64_t)k * L > pool.cap || L == 0) {
-        if (lane == 0) {
-            ctl.status |= kErrCapacity;
-            tr.ctl[t] = ctl;
-        }
-        return;
-    }
     const int depth = r.depth;
+    const int k = r.k;
     const int32_t *gp = tr.path + (size_t)t * kMaxDepth;
     const int pn_lo = lane <= depth ? gp[lane] : 0;
     const int pn_hi = lane + 64 <= depth ? gp[lane + 64] : 0;
-    float w_lo = lane <= depth ? pool.w[base + pn_lo] : 0.0f;
-    float w_hi = lane + 64 <= depth ? pool.w[base + pn_hi] : 0.0f;
-    const int copies = per_copy ? k : 1;
-    for (int j = 0; j < copies; ++j) {
-        const int64_t row = per_copy ? (int64_t)rowbase[slot] + j : (int64_t)slot;
-        const float *pol = policy + row * pld;
-        const float p0 = l0 ? pol[lane] : 0.0f;
-        const float p1 = l1 ? pol[64 + lane] : 0.0f;
-        // sequential f32 sum over legal actions in ascending order (uttt_mcts.cpp:144-152)
-        float sum = 0.0f;
-        for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
-        for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
-        const float un = 1.0f / (float)L;
-        const float q0 = sum > 0 ? p0 / sum : un;
-        const float q1 = sum > 0 ? p1 / sum : un;
-        const int reps = per_copy ? 1 : k;
-        for (int rj = 0; rj < reps; ++rj) {
-            const int blk = nb + (j + rj) * L;
+    int L = 0;
+    const int nodes_before = ctl.node_count;
+    if (!per_copy) {
+        const float *pol = policy + (int64_t)slot * pld;
+        const float v = value[(int64_t)slot * vld];
+        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, pol, v, ctl.node_count)) {
+            if (lane == 0) {
+                ctl.status |= kErrCapacity;
+                tr.ctl[t] = ctl;
+            }
+            return;
+        }
+        cache_insert(cache, s, pol, v);
+        L = (ctl.node_count - nodes_before) / k;
+    } else {
+        // the reference's exact call pattern: k results, one per queued copy, applied in order
+        uint32_t m[3];
+        legal_mask(s, m);
+        const bool l0 = bit_of(m, lane) != 0u;
+        const bool l1 = lane < 17 && bit_of(m, 64 + lane) != 0u;
+        const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
+        L = __popcll(b0) + __popcll(b1);
+        const int i0 = __popcll(b0 & lanes_below());
+        const int i1 = __popcll(b0) + __popcll(b1 & lanes_below());
+        const int nb = ctl.node_count;
+        if ((int64_t)nb + (int64_t)k * L > pool.cap || L == 0) {
+            if (lane == 0) {
+                ctl.status |= kErrCapacity;
+                tr.ctl[t] = ctl;
+            }
+            return;
+        }
+        float w_lo = lane <= depth ? pool.w[base + pn_lo] : 0.0f;
+        float w_hi = lane + 64 <= depth ? pool.w[base + pn_hi] : 0.0f;
+        for (int j = 0; j < k; ++j) {
+            const int64_t row = (int64_t)rowbase[slot] + j;
+            const float *pol = policy + row * pld;
+            const float p0 = l0 ? pol[lane] : 0.0f;
+            const float p1 = l1 ? pol[64 + lane] : 0.0f;
+            float sum = 0.0f;
+            for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
+            for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+            const float un = 1.0f / (float)L;
+            const float q0 = sum > 0 ? p0 / sum : un;
+            const float q1 = sum > 0 ? p1 / sum : un;
+            const size_t blk = base + nb + (size_t)j * L;
             if (l0) {
-                pool.n[base + blk + i0] = 0;
-                pool.w[base + blk + i0] = 0.0f;
-                pool.p[base + blk + i0] = q0;
-                pool.link[base + blk + i0] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
+                pool.n[blk + i0] = 0;
+                pool.w[blk + i0] = 0.0f;
+                pool.p[blk + i0] = q0;
+                pool.link[blk + i0] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
             }
             if (l1) {
-                pool.n[base + blk + i1] = 0;
-                pool.w[base + blk + i1] = 0.0f;
-                pool.p[base + blk + i1] = q1;
-                pool.link[base + blk + i1] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
+                pool.n[blk + i1] = 0;
+                pool.w[blk + i1] = 0.0f;
+                pool.p[blk + i1] = q1;
+                pool.link[blk + i1] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
             }
-        }
-        // backpropagate (uttt_mcts.cpp:47-54) this copy's value
-        const float v = value[row * vld];
-        const int reps_b = per_copy ? 1 : k;
-        for (int rj = 0; rj < reps_b; ++rj) {
+            const float v = value[row * vld];
             if (lane <= depth) w_lo += ((depth - lane) & 1) ? -v : v;
             if (lane + 64 <= depth) w_hi += ((depth - lane - 64) & 1) ? -v : v;
         }
-    }
-    if (lane <= depth) {
-        pool.w[base + pn_lo] = w_lo;
-        pool.n[base + pn_lo] += k;
-    }
-    if (lane + 64 <= depth) {
-        pool.w[base + pn_hi] = w_hi;
-        pool.n[base + pn_hi] += k;
+        if (lane <= depth) {
+            pool.w[base + pn_lo] = w_lo;
+            pool.n[base + pn_lo] += k;
+        }
+        if (lane + 64 <= depth) {
+            pool.w[base + pn_hi] = w_hi;
+            pool.n[base + pn_hi] += k;
+        }
+        if (lane == 0) {
+            const uint2 old = pool.link[base + r.node];
+            pool.link[base + r.node] =
+                make_uint2((uint32_t)nb, pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y)));
+        }
+        ctl.node_count = nb + k * L;
     }
     if (lane == 0) {
-        const uint2 old = pool.link[base + r.node];
-        pool.link[base + r.node] = make_uint2((uint32_t)nb, pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y)));
-        ctl.node_count = nb + k * L;
         ctl.sims_done += k;
         tr.ctl[t] = ctl;
         if (bytes_ctr) {
+            const int copies = per_copy ? k : 1;
             const unsigned long long b = 20ull * (unsigned long long)(k * L) + 81ull * 4ull * copies + 4ull * copies +
                                          8ull + 16ull * (unsigned long long)(depth + 1);
             atomicAdd(bytes_ctr, b);
@@ -833,6 +1009,12 @@ struct uttt_engine {
     // self-play
     SelfPlay sp{};
     int64_t sp_arena_used = 0;
+    // evaluation cache (off unless uttt_engine_set_cache)
+    EvalCache cache{};
+    int cache_log2 = 0;
+    int cache_clear_every = 0;
+    int64_t moves = 0;
+    unsigned long long *d_cache_ctr = nullptr;
     // telemetry
     bool timing = false;
     unsigned long long *d_bytes = nullptr;  // [kKernelCount]
@@ -1005,7 +1187,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
         (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 1)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
-        (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)))
+        (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)) ||
+        (rc = alloc_n(e, &e->d_cache_ctr, 4)))
         return fail(rc);
     if (hipHostMalloc((void **)&e->h_count, sizeof(int32_t) * 4, hipHostMallocDefault) != hipSuccess) {
         set_error("hipHostMalloc failed");
@@ -1013,6 +1196,7 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     }
     if (hipMemsetAsync(e->tr.ctl, 0, sizeof(TreeCtl) * max_trees, e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess) {
         set_error("engine init memset failed");
         return fail(UTTT_ERR_HIP);
@@ -1032,6 +1216,9 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     if (e->d_pol_scratch) (void)hipFree(e->d_pol_scratch);
     if (e->d_val_scratch) (void)hipFree(e->d_val_scratch);
     if (e->d_rowbase) (void)hipFree(e->d_rowbase);
+    if (e->cache.flag) (void)hipFree(e->cache.flag);
+    if (e->cache.key) (void)hipFree(e->cache.key);
+    if (e->cache.val) (void)hipFree(e->cache.val);
     if (e->h_count) (void)hipHostFree(e->h_count);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -1086,7 +1273,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     HIP_TRY(hipSetDevice(e->device));
     {
         TimedLaunch tl(e, kKSelect);
-        hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+        hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr, e->cache,
                            bytes_ptr(e, kKSelect));
     }
     int rc = check_launch();
@@ -1181,7 +1368,8 @@ int uttt_search_apply(uttt_engine_t *e, const float *policy, int64_t pld, const 
     }
     {
         TimedLaunch tl(e, kKApply);
-        hipLaunchKernelGGL(k_apply, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, e->pool, e->tr, dp, dpld, dv, dvld,
+        EvalCache c = per_copy ? EvalCache{} : e->cache;  // the reference call pattern bypasses the cache
+        hipLaunchKernelGGL(k_apply, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, e->pool, e->tr, c, dp, dpld, dv, dvld,
                            rowbase, per_copy ? 1 : 0, bytes_ptr(e, kKApply));
     }
     int rc = check_launch();
@@ -1304,7 +1492,8 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->selfplay = true;
     e->sp_arena_used = 0;
-    return UTTT_OK;
+    e->moves = 0;
+    return uttt_engine_cache_clear(e);  // a new run may use a new model
 }
 
 int uttt_selfplay_move_begin(uttt_engine_t *e, int32_t *n_live) {
@@ -1315,6 +1504,11 @@ int uttt_selfplay_move_begin(uttt_engine_t *e, int32_t *n_live) {
     HIP_TRY(hipSetDevice(e->device));
     const int slots = e->sp.slots;
     e->tr.n_trees = slots;
+    if (e->cache.flag && e->cache_clear_every > 0 && e->moves > 0 && e->moves % e->cache_clear_every == 0) {
+        int rc0 = uttt_engine_cache_clear(e);
+        if (rc0) return rc0;
+    }
+    e->moves++;
     // roots = the slots' current positions (Slot.state is the first member)
     std::vector<int32_t> live(slots);
     HIP_TRY(hipMemcpyAsync(live.data(), e->sp.live, sizeof(int32_t) * slots, hipMemcpyDeviceToHost, e->stream));
@@ -1436,6 +1630,55 @@ int uttt_selfplay_set_rng(uttt_engine_t *e, int32_t slot, const uint32_t key[624
     return UTTT_OK;
 }
 
+// ------------------------------------------------------- evaluation cache --
+int uttt_engine_set_cache(uttt_engine_t *e, int32_t log2_capacity, int32_t clear_every_moves) {
+    if (!e || log2_capacity < 0 || log2_capacity > 26 || clear_every_moves < 0) {
+        set_error("uttt_engine_set_cache: log2_capacity must be 0 (off) .. 26");
+        return UTTT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->cache.flag) {
+        (void)hipFree(e->cache.flag);
+        (void)hipFree(e->cache.key);
+        (void)hipFree(e->cache.val);
+        e->bytes -= (int64_t)((sizeof(uint32_t) + sizeof(uttt_state_t) + sizeof(float) * kCacheVal)
+                              << e->cache_log2);
+    }
+    e->cache = EvalCache{};
+    e->cache_log2 = log2_capacity;
+    e->cache_clear_every = clear_every_moves;
+    if (log2_capacity == 0) return UTTT_OK;
+    const size_t cap = (size_t)1 << log2_capacity;
+    HIP_TRY(hipMalloc((void **)&e->cache.flag, sizeof(uint32_t) * cap));
+    HIP_TRY(hipMalloc((void **)&e->cache.key, sizeof(uttt_state_t) * cap));
+    HIP_TRY(hipMalloc((void **)&e->cache.val, sizeof(float) * kCacheVal * cap));
+    e->bytes += (int64_t)((sizeof(uint32_t) + sizeof(uttt_state_t) + sizeof(float) * kCacheVal) * cap);
+    e->cache.mask = (uint32_t)(cap - 1);
+    e->cache.ctr = e->d_cache_ctr;
+    return uttt_engine_cache_clear(e);
+}
+
+int uttt_engine_cache_clear(uttt_engine_t *e) {
+    if (!e) return UTTT_ERR_ARG;
+    if (!e->cache.flag) return UTTT_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemsetAsync(e->cache.flag, 0, sizeof(uint32_t) * ((size_t)1 << e->cache_log2), e->stream));
+    return UTTT_OK;
+}
+
+int uttt_engine_cache_stats(uttt_engine_t *e, int64_t *hits, int64_t *misses, int64_t *inserts) {
+    if (!e) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    unsigned long long c[4];
+    HIP_TRY(hipMemcpyAsync(c, e->d_cache_ctr, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (hits) *hits = (int64_t)c[0];
+    if (misses) *misses = (int64_t)c[1];
+    if (inserts) *inserts = (int64_t)c[2];
+    return UTTT_OK;
+}
+
 // -------------------------------------------------------------- telemetry --
 int uttt_engine_set_timing(uttt_engine_t *e, int32_t enabled) {
     if (!e) return UTTT_ERR_ARG;
@@ -1466,6 +1709,7 @@ int uttt_engine_reset_stats(uttt_engine_t *e) {
         e->launches[k] = 0;
     }
     HIP_TRY(hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return UTTT_OK;
 }

@@ -26,48 +26,55 @@ namespace nn {
 constexpr int C = 128;  // DN_FILTERS
 
 // out[s][pos][c] = relu(b[c] + sum_{ch,ky,kx} w[ch*9+ky*3+kx][c] * in_ch(R+ky-1, C+kx-1))
-// one thread per (slot, position, 4 channels)
+// One workgroup per leaf: the 27x128 weights and, per output position, the
+// 27-bit mask of set input taps go to LDS; then each thread sums the weight
+// rows of the set taps for (position, 4 channels) items and stores float4s.
 __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ leaf, const int32_t *__restrict__ tree_of,
                                               int n, const float *__restrict__ w, const float *__restrict__ b,
                                               float *__restrict__ out) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    constexpr int CG = C / 4;
-    if (g >= n * 81 * CG) return;
-    const int cg = g % CG;
-    const int pos = (g / CG) % 81;
-    const int slot = g / (CG * 81);
-    const uttt_state_t s = leaf[tree_of[slot]];
-    uint32_t lm[3];
-    legal_mask(s, lm);
-    const int R = pos / 9, Cc = pos % 9;
-    float4 acc = reinterpret_cast<const float4 *>(b)[cg];
+    __shared__ float4 s_w[27 * (C / 4)];
+    __shared__ uint32_t s_mask[81];
+    const int slot = blockIdx.x;
+    const int t = threadIdx.x;
+    for (int i = t; i < 27 * (C / 4); i += 256) s_w[i] = reinterpret_cast<const float4 *>(w)[i];
+    if (t < 81) {
+        const uttt_state_t s = leaf[tree_of[slot]];
+        uint32_t lm[3];
+        legal_mask(s, lm);
+        const int R = t / 9, Cc = t % 9;
+        uint32_t m = 0u;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-        const int r = R + ky - 1;
-        if (r < 0 || r > 8) continue;
+        for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const int c = Cc + kx - 1;
-            if (c < 0 || c > 8) continue;
-            const int a = action_at(r * 9 + c);
-            const uint32_t bits[3] = {bit_of(s.own, a), bit_of(s.opp, a), bit_of(lm, a)};
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                if (bits[ch]) {
-                    const float4 wv = reinterpret_cast<const float4 *>(w + (size_t)(ch * 9 + ky * 3 + kx) * C)[cg];
-                    acc.x += wv.x;
-                    acc.y += wv.y;
-                    acc.z += wv.z;
-                    acc.w += wv.w;
-                }
+            for (int kx = 0; kx < 3; ++kx) {
+                const int r = R + ky - 1, c = Cc + kx - 1;
+                if (r < 0 || r > 8 || c < 0 || c > 8) continue;
+                const int a = action_at(r * 9 + c), tap = ky * 3 + kx;
+                m |= bit_of(s.own, a) << tap;
+                m |= bit_of(s.opp, a) << (9 + tap);
+                m |= bit_of(lm, a) << (18 + tap);
             }
-        }
+        s_mask[t] = m;
     }
-    acc.x = fmaxf(acc.x, 0.0f);
-    acc.y = fmaxf(acc.y, 0.0f);
-    acc.z = fmaxf(acc.z, 0.0f);
-    acc.w = fmaxf(acc.w, 0.0f);
-    reinterpret_cast<float4 *>(out)[g] = acc;
+    __syncthreads();
+    constexpr int CG = C / 4;
+    float4 *o = reinterpret_cast<float4 *>(out) + (size_t)slot * 81 * CG;
+    for (int i = t; i < 81 * CG; i += 256) {
+        const int pos = i / CG, cg = i % CG;
+        float4 acc = reinterpret_cast<const float4 *>(b)[cg];
+        for (uint32_t m = s_mask[pos]; m; m &= m - 1u) {
+            const float4 wv = s_w[__builtin_ctz(m) * CG + cg];
+            acc.x += wv.x;
+            acc.y += wv.y;
+            acc.z += wv.z;
+            acc.w += wv.w;
+        }
+        acc.x = fmaxf(acc.x, 0.0f);
+        acc.y = fmaxf(acc.y, 0.0f);
+        acc.z = fmaxf(acc.z, 0.0f);
+        acc.w = fmaxf(acc.w, 0.0f);
+        o[i] = acc;
+    }
 }
 
 // y = relu(x + bias[c] (+ r)), NHWC rows of C channels, float4 per thread, grid-stride.
@@ -194,8 +201,7 @@ int uttt_nn_stem(uttt_engine_t *e, const float *w, const float *b, float *out) {
         return UTTT_ERR_ARG;
     }
     if (n == 0) return UTTT_OK;
-    const int total = n * 81 * (nn::C / 4);
-    hipLaunchKernelGGL(nn::k_stem, dim3((total + 255) / 256), dim3(256), 0, st, leaf, tree_of, n, w, b, out);
+    hipLaunchKernelGGL(nn::k_stem, dim3(n), dim3(256), 0, st, leaf, tree_of, n, w, b, out);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_stem launch: %s", hipGetErrorString(r));

@@ -78,6 +78,9 @@ SIGNATURES = {
     "uttt_engine_set_timing": (ctypes.c_int, [_P, _I32]),
     "uttt_engine_kernel_stats": (ctypes.c_int, [_P, _I32, ctypes.POINTER(ctypes.c_double), _I64P, _I64P]),
     "uttt_engine_reset_stats": (ctypes.c_int, [_P]),
+    "uttt_engine_set_cache": (ctypes.c_int, [_P, _I32, _I32]),
+    "uttt_engine_cache_clear": (ctypes.c_int, [_P]),
+    "uttt_engine_cache_stats": (ctypes.c_int, [_P, _I64P, _I64P, _I64P]),
     "uttt_nn_stem": (ctypes.c_int, [_P, _P, _P, _P]),
     "uttt_nn_epilogue": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I32, _P]),
     "uttt_nn_heads": (ctypes.c_int, [_P, _P, _I32, _P, _P, _I32, _P]),

@@ -181,6 +181,19 @@ class Engine:
             ptr(val, ctypes.c_int8), ptr(hwc, ctypes.c_float) if hwc is not None else None, m, ctypes.byref(n)))
         return {"states": st, "policies": pol, "actions": act, "values": val, "inputs_hwc": hwc}
 
+    # ------------------------------------------------------- evaluation cache --
+    def set_cache(self, log2_capacity=21, clear_every_moves=32):
+        """Position -> evaluation table in HBM (0 = off). Exact for a deterministic evaluator."""
+        check(self.lib.uttt_engine_set_cache(self.h, int(log2_capacity), int(clear_every_moves)))
+
+    def cache_clear(self):
+        check(self.lib.uttt_engine_cache_clear(self.h))
+
+    def cache_stats(self):
+        h, m, i = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.uttt_engine_cache_stats(self.h, ctypes.byref(h), ctypes.byref(m), ctypes.byref(i)))
+        return {"hits": h.value, "misses": m.value, "inserts": i.value}
+
     # ------------------------------------------------------------- telemetry --
     def set_timing(self, on=True):
         check(self.lib.uttt_engine_set_timing(self.h, int(bool(on))))

@@ -54,8 +54,10 @@ class NetworkEvaluator:
 class BatchedSearch:
     """pv_mcts_scores (uttt_mcts.cpp:84-196) for many root states at once."""
 
-    def __init__(self, max_trees, max_sims=50, device=None):
+    def __init__(self, max_trees, max_sims=50, device=None, cache_log2=0):
         self.engine = Engine(max_trees, max_sims, device)
+        if cache_log2:
+            self.engine.set_cache(cache_log2, 0)
         dev = torch.device("cuda", self.engine.device)
         self.x = torch.zeros((max_trees, 3, 9, 9), dtype=torch.float32, device=dev)
         self.rounds = 0
@@ -89,8 +91,12 @@ class SelfPlay:
     (same model), independent of slot count, shard or GPU count."""
 
     def __init__(self, slots, evaluate_count=50, batch_size=8, temperature=1.0, device=None, evaluator=None,
-                 model=None):
+                 model=None, cache_log2=None, cache_clear_every=32):
         self.engine = Engine(slots, evaluate_count, device)
+        if cache_log2 is None:  # ~512 entries per slot: a 32-move window of one game's leaves
+            cache_log2 = min(21, max(12, int(math.ceil(math.log2(max(slots, 1)))) + 9))
+        if cache_log2:
+            self.engine.set_cache(cache_log2, cache_clear_every)
         self.slots = slots
         self.evaluate_count = evaluate_count
         self.batch_size = batch_size
