@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "nn", "nn-plain", "hash"], default="fused")
+    ap.add_argument("--evaluator", choices=["fused", "fused-miopen", "nn", "nn-plain", "hash"], default="fused")
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
     ap.add_argument("--cudnn-benchmark", type=int, default=1)
@@ -180,8 +180,8 @@ def main():
     sp = SelfPlay(G, S, B, 1.0, device=local, model=model, cache_log2=args.cache_log2)
     if args.evaluator == "hash":
         sp.evaluator = HashEvaluator(sp.engine)
-    elif args.evaluator == "fused":
-        sp.evaluator = FusedNetworkEvaluator(net, sp.engine)
+    elif args.evaluator in ("fused", "fused-miopen"):
+        sp.evaluator = FusedNetworkEvaluator(net, sp.engine, conv="wino" if args.evaluator == "fused" else "miopen")
 
     # NN timing (events on the stream the evaluator runs on) and useful rows
     nn_stats = {"ms": 0.0, "rows": 0, "padded_rows": 0}
@@ -279,8 +279,11 @@ def main():
                             f"{args.age} moves before warmup); one step = one move of every game",
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
                 "eval_cache_log2": args.cache_log2,
-                "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; 3x3 convs MIOpen NHWC, stem/"
-                                       "epilogues/heads as HIP kernels (csrc/nn_kernels.hip)",
+                "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
+                                       "Winograd F(2x2,3x3) f32-MFMA HIP kernel (csrc/wino_conv.hip), stem/heads "
+                                       "HIP kernels (csrc/nn_kernels.hip)",
+                              "fused-miopen": "DualNetwork 128f x16 fp32, BN folded; 3x3 convs MIOpen NHWC, stem/"
+                                              "epilogues/heads as HIP kernels (csrc/nn_kernels.hip)",
                               "nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
                               "nn-plain": "DualNetwork 128f x16 fp32 (PyTorch-ROCm/MIOpen)",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],

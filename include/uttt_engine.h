@@ -93,8 +93,8 @@ typedef struct uttt_engine uttt_engine_t;
  * exact worst case 82 + 81*max_sims nodes per tree, so it cannot overflow). */
 int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out);
 int uttt_engine_destroy(uttt_engine_t *eng);
-/* Launch everything on `stream` (a hipStream_t, e.g. torch's current stream);
- * NULL restores the engine's own stream. */
+/* Launch everything on `stream` (a hipStream_t, e.g. torch's current stream;
+ * NULL = the null stream). Until called, the engine uses a stream of its own. */
 int uttt_engine_set_stream(uttt_engine_t *eng, void *stream);
 /* Device bytes held by the engine. */
 int64_t uttt_engine_device_bytes(const uttt_engine_t *eng);

@@ -45,6 +45,15 @@ int uttt_nn_epilogue(const float *x, const float *bias, const float *residual, f
 int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float *policy, float *value,
                   int32_t softmax, void *stream);
 
+/* Residual-tower 3x3 conv (128->128, pad 1, 9x9 boards) + bias (+ residual) + ReLU as one
+ * Winograd F(2x2,3x3) f32-MFMA kernel (csrc/wino_conv.hip). x, residual, y: [n_boards][81][128]
+ * NHWC; y must not alias x or residual. u: 16*128*128 transformed weights U[xi][ci][co] = G g G^T
+ * from uttt_nn_wino_weights (host) of a folded conv weight w[128 co][128 ci][3][3], stored in the
+ * kernel's B-fragment order U[xi][ci/16][co][ci%2][(ci%16)/2]. */
+int uttt_nn_wino_weights(const float *w, float *u);
+int uttt_nn_conv3x3_wino(const float *x, const float *u, const float *bias, const float *residual, float *y,
+                         int32_t n_boards, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

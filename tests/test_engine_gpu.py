@@ -290,7 +290,13 @@ def test_fused_evaluator_matches_cpu_fp32(gpu, oracle_lib):
     roots, _ = _random_positions(oracle_lib, 300, seed=13)
     net = random_network(0, "cuda")
     bs = gpu.BatchedSearch(len(roots), 50)
-    fused = FusedNetworkEvaluator(net, bs.engine)
+    for conv in ("wino", "miopen"):
+        _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine, conv=conv))
+
+
+def _fused_vs_cpu(gpu, bs, roots, fused):
+    import torch
+    from uttt_amd.model import policy_logits, random_network
     cpu = random_network(0)
     e = bs.engine
     e.use_stream()
@@ -348,3 +354,28 @@ def test_eval_cache_is_exact(gpu, oracle_lib):
             assert np.array_equal(visits[i, :L[i]], vi), (rep, S, B, i)
     st = bs.engine.cache_stats()
     assert st["hits"] > 0 and st["inserts"] > 0
+
+
+def test_winograd_conv_matches_torch_fp32(gpu):
+    """The fused Winograd conv (+bias, +residual, ReLU) vs torch fp32 conv2d on the
+    same folded weights, for ragged board counts (tail workgroups)."""
+    import torch
+    import torch.nn.functional as F
+    from uttt_amd.model import fold_bn, random_network
+    from uttt_amd.nnfast import conv3x3_wino, wino_weights
+    net = random_network(3)
+    blk = net.residual_blocks[5]
+    w, b = fold_bn(blk.conv1, blk.bn1)
+    u = wino_weights(w).cuda()
+    w, b = w.cuda(), b.cuda()
+    g = torch.Generator().manual_seed(1)
+    for n in (1, 3, 64, 257):
+        x = torch.randn(n, 81, 128, generator=g).cuda()
+        r = torch.randn(n, 81, 128, generator=g).cuda()
+        xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
+        ref = F.conv2d(xn.double(), w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
+        for res in (None, r):
+            y = conv3x3_wino(x, u, b, res)
+            want = torch.relu(ref + (res.double() if res is not None else 0)).float()
+            err = (y - want).abs().max().item()
+            assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, res is None, err)

@@ -1227,7 +1227,10 @@ int uttt_engine_destroy(uttt_engine_t *e) {
 
 int uttt_engine_set_stream(uttt_engine_t *e, void *stream) {
     if (!e) return UTTT_ERR_ARG;
-    e->stream = stream ? (hipStream_t)stream : e->own_stream;
+    // NULL is the null (legacy default) stream — what torch.cuda.current_stream()
+    // is unless the caller made one; the engine's own stream is non-blocking and
+    // would not be ordered against it.
+    e->stream = (hipStream_t)stream;
     return UTTT_OK;
 }
 

@@ -1,9 +1,9 @@
-"""FusedNetworkEvaluator: the DualNetwork leaf evaluator with its non-GEMM parts
-as gfx950 kernels (csrc/nn_kernels.hip, include/uttt_nn.h):
+"""FusedNetworkEvaluator: the DualNetwork leaf evaluator as gfx950 kernels
+(csrc/nn_kernels.hip, csrc/wino_conv.hip, include/uttt_nn.h):
 
   leaves --k_stem--> act (n,9,9,128 NHWC, relu(conv_input+bn) applied)
-  16 x [ MIOpen conv3x3 (NHWC, no bias) -> k_epilogue(relu(. + b1))
-         MIOpen conv3x3 -> k_epilogue(relu(. + b2 + residual)) ]
+  16 x [ conv3x3 + b1 + ReLU            (conv="wino": one Winograd F(2x2,3x3) kernel
+         conv3x3 + b2 + residual + ReLU ]  conv="miopen": MIOpen NHWC conv + k_epilogue)
   --k_heads--> policy (n,81) softmax, value (n,)
 
 Replaces, per forward, the engine's NCHW encode, MIOpen's stem conv (naive /
@@ -59,8 +59,10 @@ def _p(t):
 class FusedNetworkEvaluator:
     needs_input = False
 
-    def __init__(self, net, engine, max_batch=None):
+    def __init__(self, net, engine, max_batch=None, conv="wino"):
         net = net.eval()
+        assert conv in ("wino", "miopen")
+        self.conv = conv
         self.engine = engine
         self.lib = _lib.load()
         dev = torch.device("cuda", engine.device)
@@ -77,6 +79,15 @@ class FusedNetworkEvaluator:
                 self.blocks.append((w1.to(dev).contiguous(memory_format=cl), b1.to(dev),
                                     w2.to(dev).contiguous(memory_format=cl), b2.to(dev)))
             self.heads = pack_heads(net, dev)
+            if conv == "wino":
+                self.wino = []
+                for b in net.residual_blocks:
+                    pair = []
+                    for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
+                        w, bb = fold_bn(cv, bn)
+                        pair += [wino_weights(w).to(dev), bb.to(dev)]
+                    self.wino.append(tuple(pair))
+                self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
         self.act = torch.zeros((self.max_batch, 9, 9, 128), dtype=torch.float32, device=dev)
         self.policy = torch.zeros((self.max_batch, 81), dtype=torch.float32, device=dev)
         self.value = torch.zeros((self.max_batch,), dtype=torch.float32, device=dev)
@@ -88,6 +99,8 @@ class FusedNetworkEvaluator:
     @torch.no_grad()
     def forward(self, n, softmax=True):
         """Evaluate the engine's n pending leaves; returns (policy or logits (n,81), value (n,))."""
+        if self.conv == "wino":
+            return self._forward_wino(n, softmax)
         stream = torch.cuda.current_stream(self.engine.device).cuda_stream
         nb = _bucket(n, self.max_batch)
         check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(self.act)))
@@ -103,5 +116,37 @@ class FusedNetworkEvaluator:
                                      1 if softmax else 0, ctypes.c_void_p(stream)))
         return self.policy[:n], self.value[:n]
 
+    def _forward_wino(self, n, softmax):
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.engine.device).cuda_stream)
+        x, t, y = self.buf
+        check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(x)))
+        for u1, b1, u2, b2 in self.wino:
+            check(self.lib.uttt_nn_conv3x3_wino(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
+            check(self.lib.uttt_nn_conv3x3_wino(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
+            x, y = y, x
+        check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
+                                     1 if softmax else 0, stream))
+        return self.policy[:n], self.value[:n]
+
     def __call__(self, x, n):
         return self.forward(n, True)
+
+
+def wino_weights(w):
+    """Folded conv weight (128,128,3,3) -> Winograd U (16,128,128) [xi][ci][co] (host, double precision)."""
+    import numpy as np
+    wc = np.ascontiguousarray(w.detach().float().cpu().numpy())
+    u = np.zeros((16, 128, 128), np.float32)
+    lib = _lib.load()
+    check(lib.uttt_nn_wino_weights(wc.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                   u.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return torch.from_numpy(u)
+
+
+def conv3x3_wino(x, u, bias, residual=None):
+    """Test/utility wrapper: x (n,81,128) f32 cuda -> relu(conv3x3(x) + bias (+ residual))."""
+    y = torch.empty_like(x)
+    lib = _lib.load()
+    check(lib.uttt_nn_conv3x3_wino(_p(x), _p(u), _p(bias), _p(residual) if residual is not None else None, _p(y),
+                                   x.shape[0], ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return y
