@@ -37,6 +37,9 @@ def nn_macs():
 
 
 NN_FLOP_PER_STATE = 2 * nn_macs()  # 0.765 GFLOP per evaluated position
+# residual-tower MFMA flops actually executed per board / direct-equivalent flops per state
+TOWER_MFMA_FRACTION = {"fused": 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,          # F(3x3,3x3)
+                       "fused-wino2": 32 * 25 * 16 * 128 * 128 * 2 / NN_FLOP_PER_STATE}  # F(2x2,3x3)
 
 
 def parse():
@@ -47,7 +50,8 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "fused-miopen", "nn", "nn-plain", "hash"], default="fused")
+    ap.add_argument("--evaluator", choices=["fused", "fused-wino2", "fused-miopen", "nn", "nn-plain", "hash"],
+                    default="fused")
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
     ap.add_argument("--cudnn-benchmark", type=int, default=1)
@@ -180,8 +184,9 @@ def main():
     sp = SelfPlay(G, S, B, 1.0, device=local, model=model, cache_log2=args.cache_log2)
     if args.evaluator == "hash":
         sp.evaluator = HashEvaluator(sp.engine)
-    elif args.evaluator in ("fused", "fused-miopen"):
-        sp.evaluator = FusedNetworkEvaluator(net, sp.engine, conv="wino" if args.evaluator == "fused" else "miopen")
+    elif args.evaluator.startswith("fused"):
+        conv = {"fused": "wino3", "fused-wino2": "wino", "fused-miopen": "miopen"}[args.evaluator]
+        sp.evaluator = FusedNetworkEvaluator(net, sp.engine, conv=conv)
 
     # NN timing (events on the stream the evaluator runs on) and useful rows
     nn_stats = {"ms": 0.0, "rows": 0, "padded_rows": 0}
@@ -280,8 +285,11 @@ def main():
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
                 "eval_cache_log2": args.cache_log2,
                 "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
-                                       "Winograd F(2x2,3x3) f32-MFMA HIP kernel (csrc/wino_conv.hip), stem/heads "
+                                       "Winograd F(3x3,3x3) f32-MFMA HIP kernel (csrc/wino3_conv.hip), stem/heads "
                                        "HIP kernels (csrc/nn_kernels.hip)",
+                              "fused-wino2": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
+                                             "Winograd F(2x2,3x3) f32-MFMA HIP kernel (csrc/wino_conv.hip), stem/heads "
+                                             "HIP kernels (csrc/nn_kernels.hip)",
                               "fused-miopen": "DualNetwork 128f x16 fp32, BN folded; 3x3 convs MIOpen NHWC, stem/"
                                               "epilogues/heads as HIP kernels (csrc/nn_kernels.hip)",
                               "nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
@@ -306,6 +314,10 @@ def main():
                 "ms": round(nn_stats["ms"], 2), "share_of_step": round(nn_stats["ms"] / 1e3 / elapsed, 4),
                 "achieved_tflops": round(nn_tflops, 2), "peak_tflops": FP32_PEAK_TFLOPS,
                 "frac": round(nn_tflops / FP32_PEAK_TFLOPS, 4),
+                "flops_basis": "direct-conv equivalent, 2 x MACs of dual_network.py per evaluated row "
+                               "(Winograd kernels execute fewer MFMA flops; see mfma_executed_tflops)",
+                "mfma_executed_tflops": (round(nn_tflops * TOWER_MFMA_FRACTION[args.evaluator], 2)
+                                         if args.evaluator in TOWER_MFMA_FRACTION else None),
             },
             "breakdown_ms": {"select": round(sel_ms, 2), "apply": round(app["ms"], 2), "encode": round(enc["ms"], 2),
                              "scan": round(scan["ms"], 2), "move_end": round(mend["ms"], 2),

@@ -54,6 +54,14 @@ int uttt_nn_wino_weights(const float *w, float *u);
 int uttt_nn_conv3x3_wino(const float *x, const float *u, const float *bias, const float *residual, float *y,
                          int32_t n_boards, void *stream);
 
+/* The same conv as Winograd F(3x3,3x3) (csrc/wino3_conv.hip): a 9x9 board is exactly 3x3 tiles
+ * of 3x3 outputs, 25 transform points (Toom-Cook on {0,1,-1,2,inf}). u: 25*128*128 floats,
+ * U[xi][ci][co] = G g G^T from uttt_nn_wino3_weights, stored as U[xi][ci/16][co][ci%4][(ci%16)/4].
+ * Same argument rules as uttt_nn_conv3x3_wino. */
+int uttt_nn_wino3_weights(const float *w, float *u);
+int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, const float *residual, float *y,
+                          int32_t n_boards, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -290,7 +290,7 @@ def test_fused_evaluator_matches_cpu_fp32(gpu, oracle_lib):
     roots, _ = _random_positions(oracle_lib, 300, seed=13)
     net = random_network(0, "cuda")
     bs = gpu.BatchedSearch(len(roots), 50)
-    for conv in ("wino", "miopen"):
+    for conv in ("wino3", "wino", "miopen"):
         _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine, conv=conv))
 
 
@@ -362,20 +362,21 @@ def test_winograd_conv_matches_torch_fp32(gpu):
     import torch
     import torch.nn.functional as F
     from uttt_amd.model import fold_bn, random_network
-    from uttt_amd.nnfast import conv3x3_wino, wino_weights
+    from uttt_amd.nnfast import conv3x3_wino, wino3_weights, wino_weights
     net = random_network(3)
     blk = net.residual_blocks[5]
     w, b = fold_bn(blk.conv1, blk.bn1)
-    u = wino_weights(w).cuda()
+    us = {False: wino_weights(w).cuda(), True: wino3_weights(w).cuda()}
     w, b = w.cuda(), b.cuda()
     g = torch.Generator().manual_seed(1)
-    for n in (1, 3, 64, 257):
+    for n in (1, 3, 4, 5, 64, 257, 1000):
         x = torch.randn(n, 81, 128, generator=g).cuda()
         r = torch.randn(n, 81, 128, generator=g).cuda()
         xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
         ref = F.conv2d(xn.double(), w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
-        for res in (None, r):
-            y = conv3x3_wino(x, u, b, res)
-            want = torch.relu(ref + (res.double() if res is not None else 0)).float()
-            err = (y - want).abs().max().item()
-            assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, res is None, err)
+        for f3 in (False, True):
+            for res in (None, r):
+                y = conv3x3_wino(x, us[f3], b, res, f3=f3)
+                want = torch.relu(ref + (res.double() if res is not None else 0)).float()
+                err = (y - want).abs().max().item()
+                assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, f3, res is None, err)

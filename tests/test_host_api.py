@@ -145,3 +145,36 @@ def test_winograd_algebra_matches_direct_conv(engine_lib):
         for kx in range(3):
             direct += np.einsum("rsc,oc->rso", xp[ky:ky + 9, kx:kx + 9], w[:, :, ky, kx].astype(np.float64))
     assert np.abs(y[:9, :9] - direct).max() < 1e-4 * np.abs(direct).max()
+
+
+def test_winograd3_algebra_matches_direct_conv(engine_lib):
+    """Winograd F(3x3,3x3) as k_wino3_conv computes it (U from uttt_nn_wino3_weights;
+    V = B^T d B on the 5x5 windows of the zero-padded board; Y = A^T (U . V) A on
+    3x3 tiles of 3x3 outputs, nothing cropped) equals the direct 3x3 conv."""
+    import ctypes
+    rng = np.random.RandomState(1)
+    w = rng.randn(128, 128, 3, 3).astype(np.float32)
+    u = np.zeros((25, 128, 128), np.float32)
+    fp = ctypes.POINTER(ctypes.c_float)
+    assert engine_lib.uttt_nn_wino3_weights(w.ctypes.data_as(fp), u.ctypes.data_as(fp)) == 0
+    # stored order U[xi][ci/16][co][ci%4][(ci%16)/4] -> U[xi][ci][co]
+    u = u.reshape(25, 8, 128, 4, 4).transpose(0, 1, 4, 3, 2).reshape(25, 128, 128)
+    BT = np.array([[2, -1, -2, 1, 0], [0, -2, -1, 1, 0], [0, 2, -3, 1, 0], [0, -1, 0, 1, 0], [0, 2, -1, -2, 1]],
+                  np.float64)
+    AT = np.array([[1, 1, 1, 1, 0], [0, 1, -1, 2, 0], [0, 1, 1, 4, 1]], np.float64)
+    x = rng.randn(9, 9, 128)
+    xp = np.zeros((11, 11, 128))
+    xp[1:10, 1:10] = x
+    y = np.zeros((9, 9, 128))
+    U = u.astype(np.float64).reshape(5, 5, 128, 128)
+    for ty in range(3):
+        for tx in range(3):
+            d = xp[3 * ty:3 * ty + 5, 3 * tx:3 * tx + 5]
+            V = np.einsum("ui,ijc,vj->uvc", BT, d, BT)
+            M = np.einsum("uvc,uvco->uvo", V, U)
+            y[3 * ty:3 * ty + 3, 3 * tx:3 * tx + 3] = np.einsum("au,uvo,bv->abo", AT, M, AT)
+    direct = np.zeros((9, 9, 128))
+    for ky in range(3):
+        for kx in range(3):
+            direct += np.einsum("rsc,oc->rso", xp[ky:ky + 9, kx:kx + 9], w[:, :, ky, kx].astype(np.float64))
+    assert np.abs(y - direct).max() < 1e-5 * np.abs(direct).max()

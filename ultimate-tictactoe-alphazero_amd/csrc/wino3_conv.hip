@@ -1,0 +1,459 @@
+// wino3_conv.hip — the residual tower's 3x3 convolution (dual_network.py:28-45,
+// 128 -> 128 channels, stride 1, pad 1, on 9x9 boards) as Winograd F(3x3, 3x3)
+// with f32 MFMA, bias + residual + ReLU fused into the epilogue.
+//
+// A 9x9 board is exactly 3x3 tiles of 3x3 outputs (5x5 input windows), so no
+// output is computed and thrown away: 9 tiles x 25 transform points = 225
+// MACs per (board, ci, co) against 400 for F(2x2,3x3) (5x5 tiles of 2x2, 19
+// outputs cropped) and 729 for the direct form.
+//
+//   V = B^T d B     d: 5x5 input window of a tile, per input channel
+//   M = V (.) U     per transform point xi (25): a [tiles x 128] x [128 x 128] GEMM
+//   Y = A^T M A     3x3 outputs of the tile
+// Toom-Cook points {0, 1, -1, 2, inf} (derivation and fp32 error study:
+// DESIGN.md §4); U = G g G^T precomputed per weight on the host in double.
+// Every transform coefficient is a small integer (B^T, A^T) so V and the fold
+// cost adds and exact power-of-two / small-integer scalings; products run on
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chain) with f32 accumulation.
+//
+// Workgroup = 8 waves = 32 tiles (~3.6 boards) x 128 output channels; wave w
+// owns output channels 16w..16w+15 for all 32 tiles (two 16-row MFMA blocks
+// sharing one B fragment). Per 16-channel chunk c (a phase between barriers):
+// chunk c+1 is transformed into the other V buffer while chunk c's 25 point
+// GEMMs run (the two waves of a SIMD take these in opposite order), and chunk
+// c+2's inputs are in flight to registers. M of each point is folded (row
+// half of A^T M A) into fifteen accumulators right after its MFMA chain; the
+// column half runs once in the epilogue.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "uttt_nn.h"
+
+namespace uttt {
+void set_error(const char *fmt, ...);
+
+namespace wino3 {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int C = 128;           // channels in and out
+constexpr int NP = 25;           // transform points
+constexpr int WT = 32;           // tiles per workgroup
+constexpr int KC = 16;           // input channels per chunk
+constexpr int NCH = C / KC;      // chunks
+constexpr int NB = 5;            // boards a 32-tile window can touch (9 tiles per board)
+constexpr int PB = 121;          // a board staged zero-padded to 11x11: windows need no bounds masks
+constexpr int XS = NB * PB;      // staged input floats per channel
+constexpr int NT = 512;          // threads (8 waves)
+constexpr int VB = NP * (KC / 4) * 64 * 2;  // floats per V buffer: [xi][ks][q][m][rt]
+
+// Toom-Cook F(3,3) on {0, 1, -1, 2, inf}
+__host__ __device__ constexpr int bt(int a, int i) {
+    constexpr int m[5][5] = {{2, -1, -2, 1, 0}, {0, -2, -1, 1, 0}, {0, 2, -3, 1, 0}, {0, -1, 0, 1, 0}, {0, 2, -1, -2, 1}};
+    return m[a][i];
+}
+__host__ __device__ constexpr int at(int a, int u) {
+    constexpr int m[3][5] = {{1, 1, 1, 1, 0}, {0, 1, -1, 2, 0}, {0, 1, 1, 4, 1}};
+    return m[a][u];
+}
+
+// The output transform is applied in two halves. Per point xi = (u, v) the
+// MFMA result M (both 16-row blocks, 8 floats per lane) is folded into the
+// row-transformed accumulators S[a][v] += A^T[a][u] * M; the column half
+// Y[a][b] = sum_v S[a][v] A^T[b][v] runs once, in the epilogue. 8-wide vectors
+// so the fold issues as v_pk_add_f32 / v_pk_fma_f32.
+template <int K>
+__device__ __forceinline__ void fold(floatx8 &s, const floatx8 &m) {
+    if constexpr (K == 1) s += m;
+    else if constexpr (K == -1) s -= m;
+    else if constexpr (K != 0) s = __builtin_elementwise_fma(floatx8((float)K), m, s);  // K*m exact (K = 2, 4)
+}
+
+template <int XI>
+__device__ __forceinline__ void fold_xi(floatx8 (&S)[15], const floatx8 &m) {
+    constexpr int u = XI / 5, v = XI % 5;
+    fold<at(0, u)>(S[0 * 5 + v], m);
+    fold<at(1, u)>(S[1 * 5 + v], m);
+    fold<at(2, u)>(S[2 * 5 + v], m);
+}
+
+// U stored in B-fragment order U[xi][chunk][co][q][ks] (ci = chunk*16 + 4ks + q):
+// a lane's 4 values of one point are 16 contiguous bytes.
+__device__ __forceinline__ floatx4 load_b(rsrc_t u, int xi, int chunk, int voff) {
+    const int soff = (xi * NCH + chunk) * (C * KC) * 4;
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(u, voff, soff, 0));
+}
+
+// A fragments of one point: av[ks] = (V[tile m][ci 4ks+q], V[tile 16+m][ci 4ks+q])
+__device__ __forceinline__ void load_a(floatx2 (&av)[KC / 4], const floatx2 *__restrict__ sv, int xi) {
+#pragma unroll
+    for (int ks = 0; ks < KC / 4; ++ks) av[ks] = sv[(xi * (KC / 4) + ks) * 64];
+}
+
+// Point loop, software-pipelined: B (L2) three points ahead, A (LDS) two points ahead.
+template <int XI>
+__device__ __forceinline__ floatx4 load_b_ahead(rsrc_t u, int chunk, int voff) {
+    if constexpr (XI < NP) return load_b(u, XI, chunk, voff);
+    else return load_b(u, XI - NP, (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
+}
+
+// The fold of point XI-1 is issued after point XI's MFMAs, so it never waits
+// on a just-issued chain and the next point's MFMAs follow without a bubble.
+template <int XI, int MODE>
+__device__ __forceinline__ void xi_loop(floatx8 (&S)[15], const floatx2 *__restrict__ sv, rsrc_t u, floatx4 &b0,
+                                        floatx4 &b1, floatx4 &b2, floatx2 (&a0)[KC / 4], floatx2 (&a1)[KC / 4],
+                                        floatx8 &mprev, int chunk, int voff) {
+    if constexpr (XI <= NP) {
+        floatx8 m;
+        if constexpr (XI < NP) {
+            const floatx4 b3 = load_b_ahead<XI + 3>(u, chunk, voff);
+            floatx2 a2[KC / 4];
+            if constexpr (XI + 2 < NP) load_a(a2, sv, XI + 2);
+            __builtin_amdgcn_sched_barrier(0);  // keep the prefetches at the top (the scheduler sinks them to their use)
+            floatx4 m0 = {}, m1 = {};
+#pragma unroll
+            for (int ks = 0; ks < KC / 4; ++ks) {
+                m0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].x, b0[ks], m0, 0, 0, 0);
+                m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].y, b0[ks], m1, 0, 0, 0);
+            }
+            m = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+            b0 = b1;
+            b1 = b2;
+            b2 = b3;
+#pragma unroll
+            for (int ks = 0; ks < KC / 4; ++ks) {
+                a0[ks] = a1[ks];
+                a1[ks] = a2[ks];
+            }
+        }
+        if constexpr (XI > 0) {
+            if constexpr ((MODE & 3) == 3) S[0] += mprev;
+            else fold_xi<XI - 1>(S, mprev);
+            // the fold must retire here: left alone, the compiler sinks every fold
+            // below the last point and keeps 25 live M pairs (spills)
+            asm volatile("" : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]),
+                         "+v"(S[7]), "+v"(S[8]), "+v"(S[9]), "+v"(S[10]), "+v"(S[11]), "+v"(S[12]), "+v"(S[13]),
+                         "+v"(S[14]));
+        }
+        if constexpr (XI < NP) {
+            mprev = m;
+            xi_loop<XI + 1, MODE>(S, sv, u, b0, b1, b2, a0, a1, mprev, chunk, voff);
+        }
+    }
+}
+
+constexpr int XF4 = NB * 81 * (KC / 4);   // float4s staged per chunk (1620)
+constexpr int XPT = (XF4 + NT - 1) / NT;  // per thread (4)
+
+__device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restrict__ x, int b0, int n_boards, int c0,
+                                       int tid) {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+        const int i = tid + k * NT;
+        xr[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (i < XF4) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const int b = b0 + bp / 81;
+            if (b < n_boards) xr[k] = reinterpret_cast<const float4 *>(x + ((size_t)b * 81 + bp % 81) * C + c0)[q];
+        }
+    }
+}
+
+__device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&xr)[XPT], int tid) {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+        const int i = tid + k * NT;
+        if (i < XF4) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const int pos = bp % 81, sp = (bp / 81) * PB + (pos / 9 + 1) * 11 + pos % 9 + 1;
+            sX[(4 * q + 0) * XS + sp] = xr[k].x;
+            sX[(4 * q + 1) * XS + sp] = xr[k].y;
+            sX[(4 * q + 2) * XS + sp] = xr[k].z;
+            sX[(4 * q + 3) * XS + sp] = xr[k].w;
+        }
+    }
+}
+
+// V = B^T d B for (tile, ci) items it = t0l .. WT*KC step `step`, written as
+// V[xi][ks][q][m][rt] (tile = 16rt + m, ci = 4ks + q): one ds_read_b64 per lane
+// then yields both 16-row A fragments of a k-step.
+// Boards past n_boards are staged as zeros, so their (discarded) tiles need no mask either.
+__device__ __forceinline__ void transform(float *__restrict__ sv, const float *__restrict__ sX, int t0, int b0,
+                                          int first, int step) {
+    for (int it = first; it < WT * KC; it += step) {
+        const int tl = it % WT, ci = it / WT;
+        const int T = t0 + tl;
+        const int tt = T % 9, ty = tt / 3, tx = tt % 3;
+        const float *xs = sX + ci * XS + (T / 9 - b0) * PB + 3 * ty * 11 + 3 * tx;
+        float d[5][5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[i][j] = xs[i * 11 + j];
+        float t[5][5];
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                float s = 0.0f;
+                bool first_term = true;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    if (bt(a, i) == 0) continue;
+                    const float term = bt(a, i) == 1 ? d[i][j] : bt(a, i) == -1 ? -d[i][j] : (float)bt(a, i) * d[i][j];
+                    s = first_term ? term : s + term;
+                    first_term = false;
+                }
+                t[a][j] = s;
+            }
+        float *vs = sv + ((ci >> 2) * 64 + (ci & 3) * 16 + (tl & 15)) * 2 + (tl >> 4);
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) {
+                float s = 0.0f;
+                bool first_term = true;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    if (bt(b, j) == 0) continue;
+                    const float term = bt(b, j) == 1 ? t[a][j] : bt(b, j) == -1 ? -t[a][j] : (float)bt(b, j) * t[a][j];
+                    s = first_term ? term : s + term;
+                    first_term = false;
+                }
+                vs[(a * 5 + b) * (KC / 4) * 64 * 2] = s;
+            }
+    }
+}
+
+// MODE (timing ablations only; 0 in the product): 1 skip the input transform,
+// 2 skip the point GEMMs, 3 skip the output-transform fold; +4 adds clock
+// stamps (s_memtime / s_memrealtime) into g_clk / g_phase.
+__device__ unsigned long long g_clk[4096][2];
+// MODE 4 phase stamps (core clocks) of workgroup 0..63, waves 0 and 4:
+// [wg][w][0] prologue, per chunk c: [1+4c] transform, [2+4c] gemm, [3+4c] barrier A, [4+4c] barrier B
+__device__ unsigned int g_phase[64][2][40];
+template <bool RES, int MODE = 0>
+__global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, const float *__restrict__ u,
+                                                   const float *__restrict__ bias, const float *__restrict__ res,
+                                                   float *__restrict__ y, int n_boards) {
+    __shared__ float sX[KC * XS];               // [ci][board_local*121 + padded pos], border = 0
+    __shared__ __attribute__((aligned(16))) float sV[2][VB];  // [buf][xi][ks][q][m][rt]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ntiles = n_boards * 9;
+    const int t0 = blockIdx.x * WT;
+    const int b0 = t0 / 9;
+    const int co = wv * 16 + (lane & 15);
+    unsigned long long t_core = 0, t_real = 0;
+    if ((MODE & 4) && tid == 0) {
+        t_core = __builtin_amdgcn_s_memtime();
+        t_real = __builtin_amdgcn_s_memrealtime();
+    }
+    floatx8 S[15];  // [a][v]: row-transformed accumulators, lanes 0-3 block rt=0, 4-7 rt=1
+#pragma unroll
+    for (int i = 0; i < 15; ++i) S[i] = floatx8{};
+    float4 xr[XPT];
+    const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(u), 0, NP * C * C * 4, 0x00020000);
+    const int voff = (co * 4 + (lane >> 4)) * 16;
+    // Chunk order rotated per workgroup: concurrent workgroups read different U
+    // blocks instead of all hammering the same 8 KB of L2 at once.
+    const int c_rot = blockIdx.x % NCH;
+    floatx4 b0v = load_b(ur, 0, c_rot, voff), b1v = load_b(ur, 1, c_rot, voff), b2v = load_b(ur, 2, c_rot, voff);
+
+    for (int i = tid; i < KC * XS; i += NT) sX[i] = 0.0f;  // the padding border stays zero
+    __syncthreads();
+    load_x(xr, x, b0, n_boards, c_rot * KC, tid);
+    store_x(sX, xr, tid);
+    __syncthreads();
+    if ((MODE & 3) != 1) transform(sV[0], sX, t0, b0, tid, NT);
+    load_x(xr, x, b0, n_boards, ((c_rot + 1) % NCH) * KC, tid);
+    __syncthreads();
+    store_x(sX, xr, tid);
+    __syncthreads();
+    // waves w and w+4 share a SIMD: one transforms while the other issues MFMAs
+    const int tfirst = tid & 255;
+    const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
+    unsigned long long ts = stamp ? __builtin_amdgcn_s_memtime() : 0;
+    auto mark = [&](int k) {
+        if (stamp) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            g_phase[blockIdx.x][tid >> 8][k] = (unsigned int)(t - ts);
+            ts = t;
+        }
+    };
+    if (stamp) g_phase[blockIdx.x][tid >> 8][0] = (unsigned int)(ts - t_core);
+#pragma unroll 1
+    for (int c = 0; c < NCH; ++c) {
+        const int ch = (c + c_rot) % NCH;
+        if (c + 2 < NCH) load_x(xr, x, b0, n_boards, ((ch + 2) % NCH) * KC, tid);
+        const bool tr = (MODE & 3) != 1 && c + 1 < NCH;
+        if (tr && wv < 4) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
+        if (wv < 4) mark(1 + 4 * c);
+        if constexpr ((MODE & 3) != 2) {
+            const floatx2 *sv = reinterpret_cast<const floatx2 *>(sV[c & 1]) + lane;
+            floatx2 a0[KC / 4], a1[KC / 4];
+            load_a(a0, sv, 0);
+            load_a(a1, sv, 1);
+            floatx8 mprev;
+            xi_loop<0, MODE>(S, sv, ur, b0v, b1v, b2v, a0, a1, mprev, ch, voff);
+        }
+        mark(2 + 4 * c);
+        if (tr && wv >= 4) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
+        if (wv >= 4) mark(1 + 4 * c);
+        __syncthreads();
+        mark(3 + 4 * c);
+        if (c + 2 < NCH) store_x(sX, xr, tid);
+        __syncthreads();
+        mark(4 + 4 * c);
+    }
+
+    // epilogue: Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is tile 16rt + 4(lane>>4) + r,
+    // output (3ty+a, 3tx+b); + bias, + residual, ReLU
+    floatx8 Y[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            floatx8 acc = {};
+#pragma unroll
+            for (int v = 0; v < 5; ++v) {
+                if (at(b, v) == 0) continue;
+                acc = at(b, v) == 1 ? acc + S[a * 5 + v]
+                    : at(b, v) == -1 ? acc - S[a * 5 + v]
+                                     : __builtin_elementwise_fma(floatx8((float)at(b, v)), S[a * 5 + v], acc);
+            }
+            Y[a * 3 + b] = acc;
+        }
+    if ((MODE & 4) && tid == 0 && blockIdx.x < 4096) {
+        g_clk[blockIdx.x][0] = __builtin_amdgcn_s_memtime() - t_core;
+        g_clk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime() - t_real;
+    }
+    const float bb = bias[co];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int T = t0 + 16 * rt + 4 * (lane >> 4) + r;
+            if (T >= ntiles) continue;
+            const int board = T / 9, tt = T % 9, ty = tt / 3, tx = tt % 3;
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab) {
+                const size_t idx = ((size_t)board * 81 + (3 * ty + ab / 3) * 9 + 3 * tx + ab % 3) * C + co;
+                float v = Y[ab][4 * rt + r] + bb;
+                if (RES) v += res[idx];
+                y[idx] = fmaxf(v, 0.0f);
+            }
+        }
+}
+
+}  // namespace wino3
+}  // namespace uttt
+
+using namespace uttt;
+
+extern "C" {
+
+int uttt_nn_wino3_weights(const float *w, float *u) {
+    // U[xi=(p,q)][ci][co] = (G g G^T)[p][q], g = w[co][ci][3][3], G of F(3,3) on {0,1,-1,2,inf},
+    // stored as U[xi][ci/16][co][ci%4][(ci%16)/4] (the kernel's B-fragment order)
+    if (!w || !u) {
+        set_error("uttt_nn_wino3_weights: null pointer");
+        return UTTT_ERR_ARG;
+    }
+    static const double G[5][3] = {{0.5, 0, 0},
+                                   {-0.5, -0.5, -0.5},
+                                   {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                   {1.0 / 6, 1.0 / 3, 2.0 / 3},
+                                   {0, 0, 1}};
+    using namespace wino3;
+    for (int co = 0; co < C; ++co)
+        for (int ci = 0; ci < C; ++ci) {
+            const float *g = w + ((size_t)co * C + ci) * 9;
+            double tg[5][3];
+            for (int p = 0; p < 5; ++p)
+                for (int k = 0; k < 3; ++k)
+                    tg[p][k] = G[p][0] * g[0 * 3 + k] + G[p][1] * g[1 * 3 + k] + G[p][2] * g[2 * 3 + k];
+            for (int p = 0; p < 5; ++p)
+                for (int q = 0; q < 5; ++q) {
+                    const double v = tg[p][0] * G[q][0] + tg[p][1] * G[q][1] + tg[p][2] * G[q][2];
+                    u[((((size_t)(p * 5 + q) * NCH + ci / KC) * C + co) * 4 + (ci & 3)) * 4 + (ci % KC) / 4] = (float)v;
+                }
+        }
+    return UTTT_OK;
+}
+
+int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, const float *residual, float *y,
+                          int32_t n_boards, void *stream) {
+    if (!x || !u || !bias || !y || n_boards < 0 || x == y || (residual && residual == y)) {
+        set_error("uttt_nn_conv3x3_wino3: bad arguments (output must not alias the input or residual)");
+        return UTTT_ERR_ARG;
+    }
+    if (n_boards == 0) return UTTT_OK;
+    const dim3 grid((n_boards * 9 + wino3::WT - 1) / wino3::WT);
+    if (residual)
+        hipLaunchKernelGGL(wino3::k_wino3_conv<true>, grid, dim3(wino3::NT), 0, (hipStream_t)stream, x, u, bias, residual,
+                           y, n_boards);
+    else
+        hipLaunchKernelGGL(wino3::k_wino3_conv<false>, grid, dim3(wino3::NT), 0, (hipStream_t)stream, x, u, bias, nullptr,
+                           y, n_boards);
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) {
+        set_error("k_wino3_conv launch: %s", hipGetErrorString(r));
+        return UTTT_ERR_HIP;
+    }
+    return UTTT_OK;
+}
+
+// Diagnostic (not declared in uttt_nn.h): the same launch with a timing ablation.
+int uttt_diag_wino3_ablation(const float *x, const float *u, const float *bias, float *y, int32_t n_boards,
+                             int32_t mode, void *stream) {
+    const dim3 grid((n_boards * 9 + wino3::WT - 1) / wino3::WT);
+    hipStream_t st = (hipStream_t)stream;
+    using namespace wino3;
+    switch (mode) {
+        case 1: hipLaunchKernelGGL((k_wino3_conv<false, 1>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 2: hipLaunchKernelGGL((k_wino3_conv<false, 2>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 3: hipLaunchKernelGGL((k_wino3_conv<false, 3>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3_conv<false, 4>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 5: hipLaunchKernelGGL((k_wino3_conv<false, 5>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 7: hipLaunchKernelGGL((k_wino3_conv<false, 7>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3_conv<false, 0>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards);
+    }
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+// Diagnostic: MODE-4 phase stamps, out[64][2][40] (see g_phase).
+int uttt_diag_wino3_phases(unsigned int *out) {
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(wino3::g_phase), sizeof(unsigned int) * 64 * 2 * 40) != hipSuccess)
+        return UTTT_ERR_HIP;
+    return UTTT_OK;
+}
+
+// Diagnostic: median shader clock (MHz) and median workgroup duration (us) of the last MODE-4 launch.
+int uttt_diag_wino3_clock(double *mhz, double *wg_us) {
+    static unsigned long long h[4096][2];
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(wino3::g_clk), sizeof(h)) != hipSuccess)
+        return UTTT_ERR_HIP;
+    double r[4096], d[4096];
+    int n = 0;
+    for (int i = 0; i < 4096; ++i)
+        if (h[i][1] > 0) {
+            r[n] = 100.0 * (double)h[i][0] / (double)h[i][1];
+            d[n++] = (double)h[i][1] / 100.0;
+        }
+    if (!n) return UTTT_ERR_ARG;
+    auto med = [n](double *a) {
+        for (int i = 1; i < n; ++i)
+            for (int j = i; j > 0 && a[j - 1] > a[j]; --j) { double t = a[j]; a[j] = a[j - 1]; a[j - 1] = t; }
+        return a[n / 2];
+    };
+    *mhz = med(r);
+    *wg_us = med(d);
+    return UTTT_OK;
+}
+
+}  // extern "C"

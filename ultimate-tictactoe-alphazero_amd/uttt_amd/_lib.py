@@ -86,6 +86,8 @@ SIGNATURES = {
     "uttt_nn_heads": (ctypes.c_int, [_P, _P, _I32, _P, _P, _I32, _P]),
     "uttt_nn_wino_weights": (ctypes.c_int, [_F32P, _F32P]),
     "uttt_nn_conv3x3_wino": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P]),
+    "uttt_nn_wino3_weights": (ctypes.c_int, [_F32P, _F32P]),
+    "uttt_nn_conv3x3_wino3": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P]),
 }
 
 _lib = None

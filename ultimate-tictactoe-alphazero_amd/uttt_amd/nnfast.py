@@ -2,8 +2,9 @@
 (csrc/nn_kernels.hip, csrc/wino_conv.hip, include/uttt_nn.h):
 
   leaves --k_stem--> act (n,9,9,128 NHWC, relu(conv_input+bn) applied)
-  16 x [ conv3x3 + b1 + ReLU            (conv="wino": one Winograd F(2x2,3x3) kernel
-         conv3x3 + b2 + residual + ReLU ]  conv="miopen": MIOpen NHWC conv + k_epilogue)
+  16 x [ conv3x3 + b1 + ReLU            (conv="wino3": one Winograd F(3x3,3x3) kernel,
+         conv3x3 + b2 + residual + ReLU ]  conv="wino": one Winograd F(2x2,3x3) kernel,
+                                           conv="miopen": MIOpen NHWC conv + k_epilogue)
   --k_heads--> policy (n,81) softmax, value (n,)
 
 Replaces, per forward, the engine's NCHW encode, MIOpen's stem conv (naive /
@@ -59,9 +60,9 @@ def _p(t):
 class FusedNetworkEvaluator:
     needs_input = False
 
-    def __init__(self, net, engine, max_batch=None, conv="wino"):
+    def __init__(self, net, engine, max_batch=None, conv="wino3"):
         net = net.eval()
-        assert conv in ("wino", "miopen")
+        assert conv in ("wino3", "wino", "miopen")
         self.conv = conv
         self.engine = engine
         self.lib = _lib.load()
@@ -79,13 +80,15 @@ class FusedNetworkEvaluator:
                 self.blocks.append((w1.to(dev).contiguous(memory_format=cl), b1.to(dev),
                                     w2.to(dev).contiguous(memory_format=cl), b2.to(dev)))
             self.heads = pack_heads(net, dev)
-            if conv == "wino":
+            if conv in ("wino", "wino3"):
+                wfn = wino3_weights if conv == "wino3" else wino_weights
+                self.conv_fn = self.lib.uttt_nn_conv3x3_wino3 if conv == "wino3" else self.lib.uttt_nn_conv3x3_wino
                 self.wino = []
                 for b in net.residual_blocks:
                     pair = []
                     for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
                         w, bb = fold_bn(cv, bn)
-                        pair += [wino_weights(w).to(dev), bb.to(dev)]
+                        pair += [wfn(w).to(dev), bb.to(dev)]
                     self.wino.append(tuple(pair))
                 self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
         self.act = torch.zeros((self.max_batch, 9, 9, 128), dtype=torch.float32, device=dev)
@@ -99,7 +102,7 @@ class FusedNetworkEvaluator:
     @torch.no_grad()
     def forward(self, n, softmax=True):
         """Evaluate the engine's n pending leaves; returns (policy or logits (n,81), value (n,))."""
-        if self.conv == "wino":
+        if self.conv != "miopen":
             return self._forward_wino(n, softmax)
         stream = torch.cuda.current_stream(self.engine.device).cuda_stream
         nb = _bucket(n, self.max_batch)
@@ -121,8 +124,8 @@ class FusedNetworkEvaluator:
         x, t, y = self.buf
         check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(x)))
         for u1, b1, u2, b2 in self.wino:
-            check(self.lib.uttt_nn_conv3x3_wino(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
-            check(self.lib.uttt_nn_conv3x3_wino(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
+            check(self.conv_fn(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
+            check(self.conv_fn(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
             x, y = y, x
         check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
                                      1 if softmax else 0, stream))
@@ -143,10 +146,23 @@ def wino_weights(w):
     return torch.from_numpy(u)
 
 
-def conv3x3_wino(x, u, bias, residual=None):
-    """Test/utility wrapper: x (n,81,128) f32 cuda -> relu(conv3x3(x) + bias (+ residual))."""
+def wino3_weights(w):
+    """Folded conv weight (128,128,3,3) -> Winograd F(3x3,3x3) U, 25*128*128 floats in kernel order (host, double)."""
+    import numpy as np
+    wc = np.ascontiguousarray(w.detach().float().cpu().numpy())
+    u = np.zeros((25, 128, 128), np.float32)
+    lib = _lib.load()
+    check(lib.uttt_nn_wino3_weights(wc.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                    u.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return torch.from_numpy(u)
+
+
+def conv3x3_wino(x, u, bias, residual=None, f3=False):
+    """Test/utility wrapper: x (n,81,128) f32 cuda -> relu(conv3x3(x) + bias (+ residual)).
+    f3: u is a wino3_weights() transform (F(3x3,3x3) kernel), else wino_weights() (F(2x2,3x3))."""
     y = torch.empty_like(x)
     lib = _lib.load()
-    check(lib.uttt_nn_conv3x3_wino(_p(x), _p(u), _p(bias), _p(residual) if residual is not None else None, _p(y),
-                                   x.shape[0], ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    fn = lib.uttt_nn_conv3x3_wino3 if f3 else lib.uttt_nn_conv3x3_wino
+    check(fn(_p(x), _p(u), _p(bias), _p(residual) if residual is not None else None, _p(y),
+             x.shape[0], ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return y
