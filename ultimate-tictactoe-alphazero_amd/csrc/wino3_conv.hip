@@ -62,23 +62,34 @@ __host__ __device__ constexpr int at(int a, int u) {
 }
 
 // The output transform is applied in two halves. Per point xi = (u, v) the
-// MFMA result M (both 16-row blocks, 8 floats per lane) is folded into the
-// row-transformed accumulators S[a][v] += A^T[a][u] * M; the column half
-// Y[a][b] = sum_v S[a][v] A^T[b][v] runs once, in the epilogue. 8-wide vectors
-// so the fold issues as v_pk_add_f32 / v_pk_fma_f32.
+// MFMA result M (both 16-row blocks: 8 floats per lane, four register pairs)
+// is folded into the row-transformed accumulators S[a][v] += A^T[a][u] * M;
+// the column half Y[a][b] = sum_v S[a][v] A^T[b][v] runs once, in the
+// epilogue. The fold is written as packed-f32 asm (v_pk_add_f32 /
+// v_pk_fma_f32 on aligned pairs; hipcc lowers the vector form to scalar adds)
+// and, being volatile, stays in program order right where it is issued.
+struct Acc {
+    floatx2 p[4];
+};
+
 template <int K>
-__device__ __forceinline__ void fold(floatx8 &s, const floatx8 &m) {
-    if constexpr (K == 1) s += m;
-    else if constexpr (K == -1) s -= m;
-    else if constexpr (K != 0) s = __builtin_elementwise_fma(floatx8((float)K), m, s);  // K*m exact (K = 2, 4)
+__device__ __forceinline__ void fold(Acc &s, const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(s.p[i]) : "v"(m[i]));
+        else if constexpr (K == -1) asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(s.p[i]) : "v"(m[i]));
+        else if constexpr (K == 2) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(s.p[i]) : "v"(m[i]), "v"(k2));
+        else if constexpr (K == 4) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(s.p[i]) : "v"(m[i]), "v"(k4));
+        else static_assert(K == 0, "A^T coefficients are 0, +-1, 2, 4");
+    }
 }
 
 template <int XI>
-__device__ __forceinline__ void fold_xi(floatx8 (&S)[15], const floatx8 &m) {
+__device__ __forceinline__ void fold_xi(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
     constexpr int u = XI / 5, v = XI % 5;
-    fold<at(0, u)>(S[0 * 5 + v], m);
-    fold<at(1, u)>(S[1 * 5 + v], m);
-    fold<at(2, u)>(S[2 * 5 + v], m);
+    fold<at(0, u)>(S[0 * 5 + v], m, k2, k4);
+    fold<at(1, u)>(S[1 * 5 + v], m, k2, k4);
+    fold<at(2, u)>(S[2 * 5 + v], m, k2, k4);
 }
 
 // U stored in B-fragment order U[xi][chunk][co][q][ks] (ci = chunk*16 + 4ks + q):
@@ -104,15 +115,25 @@ __device__ __forceinline__ floatx4 load_b_ahead(rsrc_t u, int chunk, int voff) {
 // The fold of point XI-1 is issued after point XI's MFMAs, so it never waits
 // on a just-issued chain and the next point's MFMAs follow without a bubble.
 template <int XI, int MODE>
-__device__ __forceinline__ void xi_loop(floatx8 (&S)[15], const floatx2 *__restrict__ sv, rsrc_t u, floatx4 &b0,
+__device__ __forceinline__ void xi_loop(Acc (&S)[15], const floatx2 *__restrict__ sv, rsrc_t u, floatx4 &b0,
                                         floatx4 &b1, floatx4 &b2, floatx2 (&a0)[KC / 4], floatx2 (&a1)[KC / 4],
-                                        floatx8 &mprev, int chunk, int voff) {
+                                        floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff) {
     if constexpr (XI <= NP) {
-        floatx8 m;
+        floatx2 m[4];
         if constexpr (XI < NP) {
-            const floatx4 b3 = load_b_ahead<XI + 3>(u, chunk, voff);
+            floatx4 b3 = b0;
             floatx2 a2[KC / 4];
-            if constexpr (XI + 2 < NP) load_a(a2, sv, XI + 2);
+            if constexpr (MODE & 32) {
+#pragma unroll
+                for (int ks = 0; ks < KC / 4; ++ks) {
+                    a2[ks] = a0[ks];
+                    asm volatile("" : "+v"(a2[ks]));  // opaque copy: no CSE of the MFMAs
+                }
+                asm volatile("" : "+v"(b3));
+            } else {
+                b3 = load_b_ahead<XI + 3>(u, chunk, voff);
+                if constexpr (XI + 2 < NP) load_a(a2, sv, XI + 2);
+            }
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetches at the top (the scheduler sinks them to their use)
             floatx4 m0 = {}, m1 = {};
 #pragma unroll
@@ -120,7 +141,10 @@ __device__ __forceinline__ void xi_loop(floatx8 (&S)[15], const floatx2 *__restr
                 m0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].x, b0[ks], m0, 0, 0, 0);
                 m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].y, b0[ks], m1, 0, 0, 0);
             }
-            m = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+            m[0] = __builtin_shufflevector(m0, m0, 0, 1);
+            m[1] = __builtin_shufflevector(m0, m0, 2, 3);
+            m[2] = __builtin_shufflevector(m1, m1, 0, 1);
+            m[3] = __builtin_shufflevector(m1, m1, 2, 3);
             b0 = b1;
             b1 = b2;
             b2 = b3;
@@ -130,18 +154,16 @@ __device__ __forceinline__ void xi_loop(floatx8 (&S)[15], const floatx2 *__restr
                 a1[ks] = a2[ks];
             }
         }
-        if constexpr (XI > 0) {
-            if constexpr ((MODE & 3) == 3) S[0] += mprev;
-            else fold_xi<XI - 1>(S, mprev);
-            // the fold must retire here: left alone, the compiler sinks every fold
-            // below the last point and keeps 25 live M pairs (spills)
-            asm volatile("" : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]),
-                         "+v"(S[7]), "+v"(S[8]), "+v"(S[9]), "+v"(S[10]), "+v"(S[11]), "+v"(S[12]), "+v"(S[13]),
-                         "+v"(S[14]));
+        if constexpr (XI > 0 && (MODE & 64)) {
+            asm volatile("" : "+v"(mprev[0]), "+v"(mprev[1]), "+v"(mprev[2]), "+v"(mprev[3]));  // diagnostic: no fold
+        } else if constexpr (XI > 0) {
+            if constexpr ((MODE & 3) == 3) fold<1>(S[0], mprev, k2, k4);
+            else fold_xi<XI - 1>(S, mprev, k2, k4);
         }
         if constexpr (XI < NP) {
-            mprev = m;
-            xi_loop<XI + 1, MODE>(S, sv, u, b0, b1, b2, a0, a1, mprev, chunk, voff);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mprev[i] = m[i];
+            xi_loop<XI + 1, MODE>(S, sv, u, b0, b1, b2, a0, a1, mprev, k2, k4, chunk, voff);
         }
     }
 }
@@ -178,60 +200,69 @@ __device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&x
     }
 }
 
-// V = B^T d B for (tile, ci) items it = t0l .. WT*KC step `step`, written as
-// V[xi][ks][q][m][rt] (tile = 16rt + m, ci = 4ks + q): one ds_read_b64 per lane
-// then yields both 16-row A fragments of a k-step.
-// Boards past n_boards are staged as zeros, so their (discarded) tiles need no mask either.
+// V = B^T d B for item pairs (tiles m and 16+m of one input channel ci), it =
+// first .. WT/2*KC step `step`, in packed f32; V[xi][ks][q][m][rt] (ci = 4ks + q)
+// takes each pair as one ds_write_b64, and one ds_read_b64 per lane then
+// yields both 16-row A fragments of a k-step. Boards past n_boards are staged
+// as zeros, so their (discarded) tiles need no mask.
+template <int R>
+__device__ __forceinline__ floatx2 bt_row(const floatx2 (&d)[5]) {
+    floatx2 s = {0.0f, 0.0f};
+    bool first_term = true;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const int k = bt(R, i);
+        if (k == 0) continue;
+        const floatx2 term = k == 1 ? d[i] : k == -1 ? -d[i] : (float)k * d[i];
+        s = first_term ? term : s + term;
+        first_term = false;
+    }
+    return s;
+}
+
 __device__ __forceinline__ void transform(float *__restrict__ sv, const float *__restrict__ sX, int t0, int b0,
                                           int first, int step) {
-    for (int it = first; it < WT * KC; it += step) {
-        const int tl = it % WT, ci = it / WT;
-        const int T = t0 + tl;
-        const int tt = T % 9, ty = tt / 3, tx = tt % 3;
-        const float *xs = sX + ci * XS + (T / 9 - b0) * PB + 3 * ty * 11 + 3 * tx;
-        float d[5][5];
+    for (int it = first; it < (WT / 2) * KC; it += step) {
+        const int m = it % (WT / 2), ci = it / (WT / 2);
+        const float *xs[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int T = t0 + 16 * r + m;
+            const int tt = T % 9, ty = tt / 3, tx = tt % 3;
+            xs[r] = sX + ci * XS + (T / 9 - b0) * PB + 3 * ty * 11 + 3 * tx;
+        }
+        floatx2 d[5][5];
 #pragma unroll
         for (int i = 0; i < 5; ++i)
 #pragma unroll
-            for (int j = 0; j < 5; ++j) d[i][j] = xs[i * 11 + j];
-        float t[5][5];
+            for (int j = 0; j < 5; ++j) d[i][j] = floatx2{xs[0][i * 11 + j], xs[1][i * 11 + j]};
+        floatx2 t[5][5];  // t = B^T d
 #pragma unroll
-        for (int a = 0; a < 5; ++a)
+        for (int j = 0; j < 5; ++j) {
+            const floatx2 col[5] = {d[0][j], d[1][j], d[2][j], d[3][j], d[4][j]};
+            t[0][j] = bt_row<0>(col);
+            t[1][j] = bt_row<1>(col);
+            t[2][j] = bt_row<2>(col);
+            t[3][j] = bt_row<3>(col);
+            t[4][j] = bt_row<4>(col);
+        }
+        floatx2 *vs = reinterpret_cast<floatx2 *>(sv) + (ci >> 2) * 64 + (ci & 3) * 16 + m;
 #pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                float s = 0.0f;
-                bool first_term = true;
-#pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    if (bt(a, i) == 0) continue;
-                    const float term = bt(a, i) == 1 ? d[i][j] : bt(a, i) == -1 ? -d[i][j] : (float)bt(a, i) * d[i][j];
-                    s = first_term ? term : s + term;
-                    first_term = false;
-                }
-                t[a][j] = s;
-            }
-        float *vs = sv + ((ci >> 2) * 64 + (ci & 3) * 16 + (tl & 15)) * 2 + (tl >> 4);
-#pragma unroll
-        for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int b = 0; b < 5; ++b) {
-                float s = 0.0f;
-                bool first_term = true;
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    if (bt(b, j) == 0) continue;
-                    const float term = bt(b, j) == 1 ? t[a][j] : bt(b, j) == -1 ? -t[a][j] : (float)bt(b, j) * t[a][j];
-                    s = first_term ? term : s + term;
-                    first_term = false;
-                }
-                vs[(a * 5 + b) * (KC / 4) * 64 * 2] = s;
-            }
+        for (int a = 0; a < 5; ++a) {  // V = t B
+            vs[(a * 5 + 0) * (KC / 4) * 64] = bt_row<0>(t[a]);
+            vs[(a * 5 + 1) * (KC / 4) * 64] = bt_row<1>(t[a]);
+            vs[(a * 5 + 2) * (KC / 4) * 64] = bt_row<2>(t[a]);
+            vs[(a * 5 + 3) * (KC / 4) * 64] = bt_row<3>(t[a]);
+            vs[(a * 5 + 4) * (KC / 4) * 64] = bt_row<4>(t[a]);
+        }
     }
 }
 
 // MODE (timing ablations only; 0 in the product): 1 skip the input transform,
 // 2 skip the point GEMMs, 3 skip the output-transform fold; +4 adds clock
-// stamps (s_memtime / s_memrealtime) into g_clk / g_phase.
+// stamps (s_memtime / s_memrealtime) into g_clk / g_phase; +8 raises waves 4-7
+// to s_setprio 1; +16 swaps which half transforms first; +32 runs the point
+// loop on registers only (no A / B operand loads).
 __device__ unsigned long long g_clk[4096][2];
 // MODE 4 phase stamps (core clocks) of workgroup 0..63, waves 0 and 4:
 // [wg][w][0] prologue, per chunk c: [1+4c] transform, [2+4c] gemm, [3+4c] barrier A, [4+4c] barrier B
@@ -252,9 +283,12 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
         t_core = __builtin_amdgcn_s_memtime();
         t_real = __builtin_amdgcn_s_memrealtime();
     }
-    floatx8 S[15];  // [a][v]: row-transformed accumulators, lanes 0-3 block rt=0, 4-7 rt=1
+    Acc S[15];  // [a][v]: row-transformed accumulators; pairs 0-1 block rt=0, 2-3 rt=1
 #pragma unroll
-    for (int i = 0; i < 15; ++i) S[i] = floatx8{};
+    for (int i = 0; i < 15; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+    const floatx2 k2 = {2.0f, 2.0f}, k4 = {4.0f, 4.0f};
     float4 xr[XPT];
     const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(u), 0, NP * C * C * 4, 0x00020000);
     const int voff = (co * 4 + (lane >> 4)) * 16;
@@ -275,6 +309,10 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
     __syncthreads();
     // waves w and w+4 share a SIMD: one transforms while the other issues MFMAs
     const int tfirst = tid & 255;
+    if ((MODE & 8) && wv >= 4) __builtin_amdgcn_s_setprio(1);
+    // the younger half (waves 4-7) transforms first: the older half, which wins
+    // issue arbitration, starts its MFMAs at once (+2% over the reverse order)
+    const bool tr_first = (MODE & 16) ? wv < 4 : wv >= 4;
     const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
     unsigned long long ts = stamp ? __builtin_amdgcn_s_memtime() : 0;
     auto mark = [&](int k) {
@@ -290,19 +328,19 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
         const int ch = (c + c_rot) % NCH;
         if (c + 2 < NCH) load_x(xr, x, b0, n_boards, ((ch + 2) % NCH) * KC, tid);
         const bool tr = (MODE & 3) != 1 && c + 1 < NCH;
-        if (tr && wv < 4) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
-        if (wv < 4) mark(1 + 4 * c);
+        if (tr && tr_first) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
+        if (tr_first) mark(1 + 4 * c);
         if constexpr ((MODE & 3) != 2) {
             const floatx2 *sv = reinterpret_cast<const floatx2 *>(sV[c & 1]) + lane;
             floatx2 a0[KC / 4], a1[KC / 4];
             load_a(a0, sv, 0);
             load_a(a1, sv, 1);
-            floatx8 mprev;
-            xi_loop<0, MODE>(S, sv, ur, b0v, b1v, b2v, a0, a1, mprev, ch, voff);
+            floatx2 mprev[4];
+            xi_loop<0, MODE>(S, sv, ur, b0v, b1v, b2v, a0, a1, mprev, k2, k4, ch, voff);
         }
         mark(2 + 4 * c);
-        if (tr && wv >= 4) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
-        if (wv >= 4) mark(1 + 4 * c);
+        if (tr && !tr_first) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
+        if (!tr_first) mark(1 + 4 * c);
         __syncthreads();
         mark(3 + 4 * c);
         if (c + 2 < NCH) store_x(sX, xr, tid);
@@ -321,9 +359,11 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
 #pragma unroll
             for (int v = 0; v < 5; ++v) {
                 if (at(b, v) == 0) continue;
-                acc = at(b, v) == 1 ? acc + S[a * 5 + v]
-                    : at(b, v) == -1 ? acc - S[a * 5 + v]
-                                     : __builtin_elementwise_fma(floatx8((float)at(b, v)), S[a * 5 + v], acc);
+                const Acc &q = S[a * 5 + v];
+                const floatx8 sv8 = {q.p[0].x, q.p[0].y, q.p[1].x, q.p[1].y, q.p[2].x, q.p[2].y, q.p[3].x, q.p[3].y};
+                acc = at(b, v) == 1 ? acc + sv8
+                    : at(b, v) == -1 ? acc - sv8
+                                     : __builtin_elementwise_fma(floatx8((float)at(b, v)), sv8, acc);
             }
             Y[a * 3 + b] = acc;
         }
@@ -420,6 +460,13 @@ int uttt_diag_wino3_ablation(const float *x, const float *u, const float *bias, 
         case 4: hipLaunchKernelGGL((k_wino3_conv<false, 4>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 5: hipLaunchKernelGGL((k_wino3_conv<false, 5>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 7: hipLaunchKernelGGL((k_wino3_conv<false, 7>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 8: hipLaunchKernelGGL((k_wino3_conv<false, 8>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 16: hipLaunchKernelGGL((k_wino3_conv<false, 16>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 24: hipLaunchKernelGGL((k_wino3_conv<false, 24>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 33: hipLaunchKernelGGL((k_wino3_conv<false, 33>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 35: hipLaunchKernelGGL((k_wino3_conv<false, 35>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 97: hipLaunchKernelGGL((k_wino3_conv<false, 97>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 65: hipLaunchKernelGGL((k_wino3_conv<false, 65>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         default: hipLaunchKernelGGL((k_wino3_conv<false, 0>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards);
     }
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
