@@ -10,8 +10,8 @@
 //   V = B^T d B     d: 5x5 input window of a tile, per input channel
 //   M = V (.) U     per transform point xi (25): a [tiles x 128] x [128 x 128] GEMM
 //   Y = A^T M A     3x3 outputs of the tile
-// Toom-Cook points {0, 1, -1, 2, inf} (derivation and fp32 error study:
-// DESIGN.md §4); U = G g G^T precomputed per weight on the host in double.
+// Toom-Cook points {0, 1, -1, 2, inf} (fp32 error study:
+// DESIGN.md §5); U = G g G^T precomputed per weight on the host in double.
 // Every transform coefficient is a small integer (B^T, A^T) so V and the fold
 // cost adds and exact power-of-two / small-integer scalings; products run on
 // v_mfma_f32_16x16x4_f32 (exact f32 fma chain) with f32 accumulation.
