@@ -26,9 +26,8 @@ if mode & 4:
     ph = np.zeros((64, 2, 40), np.uint32)
     assert lib.uttt_diag_wino3_phases(ph.ctypes.data_as(ctypes.c_void_p)) == 0
     med = np.median(ph[8:56].astype(np.float64), axis=0)   # skip first/last launches' edge WGs
-    for w, nm in ((0, "wave0 (transform first)"), (1, "wave4 (gemm first)")):
-        print(nm, "prologue", int(med[w, 0]))
+    for w, nm in ((0, "wave0"), (1, "wave4")):
+        print(nm, "prologue", int(med[w, 0]) if w == 0 else "-")
         for c in range(8):
             t, g, ba, bb = med[w, 1 + 4 * c:5 + 4 * c]
-            first, second = ("transform", "gemm") if w == 0 else ("gemm", "transform")
-            print(f"  chunk {c}: {first} {int(t if w == 0 else g):6d}  {second} {int(g if w == 0 else t):6d}  barrierA {int(ba):6d}  store+barrierB {int(bb):6d}")
+            print(f"  chunk {c}: transform {int(t):6d}  gemm {int(g):6d}  barrierA {int(ba):6d}  store+barrierB {int(bb):6d}")

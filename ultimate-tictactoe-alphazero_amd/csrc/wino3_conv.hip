@@ -205,19 +205,20 @@ __device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&x
 // takes each pair as one ds_write_b64, and one ds_read_b64 per lane then
 // yields both 16-row A fragments of a k-step. Boards past n_boards are staged
 // as zeros, so their (discarded) tiles need no mask.
-template <int R>
-__device__ __forceinline__ floatx2 bt_row(const floatx2 (&d)[5]) {
-    floatx2 s = {0.0f, 0.0f};
-    bool first_term = true;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const int k = bt(R, i);
-        if (k == 0) continue;
-        const floatx2 term = k == 1 ? d[i] : k == -1 ? -d[i] : (float)k * d[i];
-        s = first_term ? term : s + term;
-        first_term = false;
-    }
-    return s;
+// x -> B^T x for one 5-vector of tile pairs, common subexpressions shared:
+// 9 packed ops (5 of them fma) instead of ~20 for the rows written out.
+__device__ __forceinline__ void bt5(const floatx2 (&d)[5], floatx2 (&t)[5]) {
+    const floatx2 two = {2.0f, 2.0f}, mtwo = {-2.0f, -2.0f};
+    const floatx2 e = d[3] - d[2];
+    const floatx2 f = d[1] - d[2];
+    const floatx2 t3 = d[3] - d[1];
+    const floatx2 g = d[0] - d[2];
+    const floatx2 h = d[4] - d[2];
+    t[0] = __builtin_elementwise_fma(two, g, t3);   //  2d0 - d1 - 2d2 + d3
+    t[1] = __builtin_elementwise_fma(mtwo, d[1], e); // -2d1 - d2 + d3
+    t[2] = __builtin_elementwise_fma(two, f, e);    //  2d1 - 3d2 + d3
+    t[3] = t3;                                      //  -d1 + d3
+    t[4] = __builtin_elementwise_fma(mtwo, t3, h);  //  2d1 - d2 - 2d3 + d4
 }
 
 __device__ __forceinline__ void transform(float *__restrict__ sv, const float *__restrict__ sX, int t0, int b0,
@@ -236,24 +237,22 @@ __device__ __forceinline__ void transform(float *__restrict__ sv, const float *_
         for (int i = 0; i < 5; ++i)
 #pragma unroll
             for (int j = 0; j < 5; ++j) d[i][j] = floatx2{xs[0][i * 11 + j], xs[1][i * 11 + j]};
-        floatx2 t[5][5];  // t = B^T d
+        floatx2 t[5][5];  // t = B^T d (t[a][j])
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const floatx2 col[5] = {d[0][j], d[1][j], d[2][j], d[3][j], d[4][j]};
-            t[0][j] = bt_row<0>(col);
-            t[1][j] = bt_row<1>(col);
-            t[2][j] = bt_row<2>(col);
-            t[3][j] = bt_row<3>(col);
-            t[4][j] = bt_row<4>(col);
+            floatx2 o[5];
+            bt5(col, o);
+#pragma unroll
+            for (int a = 0; a < 5; ++a) t[a][j] = o[a];
         }
         floatx2 *vs = reinterpret_cast<floatx2 *>(sv) + (ci >> 2) * 64 + (ci & 3) * 16 + m;
 #pragma unroll
         for (int a = 0; a < 5; ++a) {  // V = t B
-            vs[(a * 5 + 0) * (KC / 4) * 64] = bt_row<0>(t[a]);
-            vs[(a * 5 + 1) * (KC / 4) * 64] = bt_row<1>(t[a]);
-            vs[(a * 5 + 2) * (KC / 4) * 64] = bt_row<2>(t[a]);
-            vs[(a * 5 + 3) * (KC / 4) * 64] = bt_row<3>(t[a]);
-            vs[(a * 5 + 4) * (KC / 4) * 64] = bt_row<4>(t[a]);
+            floatx2 o[5];
+            bt5(t[a], o);
+#pragma unroll
+            for (int b = 0; b < 5; ++b) vs[(a * 5 + b) * (KC / 4) * 64] = o[b];
         }
     }
 }
@@ -261,12 +260,19 @@ __device__ __forceinline__ void transform(float *__restrict__ sv, const float *_
 // MODE (timing ablations only; 0 in the product): 1 skip the input transform,
 // 2 skip the point GEMMs, 3 skip the output-transform fold; +4 adds clock
 // stamps (s_memtime / s_memrealtime) into g_clk / g_phase; +8 raises waves 4-7
-// to s_setprio 1; +16 swaps which half transforms first; +32 runs the point
-// loop on registers only (no A / B operand loads).
+// to s_setprio 1; +16 swaps which half transforms the even chunks; +32 runs the
+// point loop on registers only (no A / B operand loads); +64 skips the fold;
+// +128 raises the transforming waves to s_setprio 3 for the transform.
 __device__ unsigned long long g_clk[4096][2];
-// MODE 4 phase stamps (core clocks) of workgroup 0..63, waves 0 and 4:
-// [wg][w][0] prologue, per chunk c: [1+4c] transform, [2+4c] gemm, [3+4c] barrier A, [4+4c] barrier B
+// MODE+4 phase stamps (core clocks) of workgroups 0..63, waves 0 and 4, first 8 chunks:
+// [wg][w][0] prologue, per chunk c: [1+4c] transform, [2+4c] gemm(+epilogue), [3+4c] barrier A, [4+4c] barrier B
 __device__ unsigned int g_phase[64][2][40];
+
+// Persistent: one workgroup per CU walks tile sets blockIdx.x, +gridDim.x, ...
+// The chunk pipeline (stage two chunks ahead, transform one ahead, GEMM) runs
+// straight across set boundaries, so only the first set pays a prologue; a
+// set's epilogue (output transform, bias, residual, ReLU, store) follows the
+// GEMMs of its last chunk.
 template <bool RES, int MODE = 0>
 __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, const float *__restrict__ u,
                                                    const float *__restrict__ bias, const float *__restrict__ res,
@@ -275,8 +281,11 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
     __shared__ __attribute__((aligned(16))) float sV[2][VB];  // [buf][xi][ks][q][m][rt]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ntiles = n_boards * 9;
-    const int t0 = blockIdx.x * WT;
-    const int b0 = t0 / 9;
+    const int nsets = (ntiles + WT - 1) / WT;
+    if ((int)blockIdx.x >= nsets) return;
+    const int my_sets = (nsets - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = my_sets * NCH;  // chunks this workgroup runs
+    auto set_t0 = [&](int g) { return ((int)blockIdx.x + (g / NCH) * (int)gridDim.x) * WT; };
     const int co = wv * 16 + (lane & 15);
     unsigned long long t_core = 0, t_real = 0;
     if ((MODE & 4) && tid == 0) {
@@ -295,28 +304,32 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
     // Chunk order rotated per workgroup: concurrent workgroups read different U
     // blocks instead of all hammering the same 8 KB of L2 at once.
     const int c_rot = blockIdx.x % NCH;
+    auto chunk_of = [&](int g) { return (g % NCH + c_rot) % NCH; };
     floatx4 b0v = load_b(ur, 0, c_rot, voff), b1v = load_b(ur, 1, c_rot, voff), b2v = load_b(ur, 2, c_rot, voff);
+    const float bb = bias[co];
 
     for (int i = tid; i < KC * XS; i += NT) sX[i] = 0.0f;  // the padding border stays zero
     __syncthreads();
-    load_x(xr, x, b0, n_boards, c_rot * KC, tid);
+    load_x(xr, x, set_t0(0) / 9, n_boards, chunk_of(0) * KC, tid);
     store_x(sX, xr, tid);
     __syncthreads();
-    if ((MODE & 3) != 1) transform(sV[0], sX, t0, b0, tid, NT);
-    load_x(xr, x, b0, n_boards, ((c_rot + 1) % NCH) * KC, tid);
+    if ((MODE & 3) != 1) transform(sV[0], sX, set_t0(0), set_t0(0) / 9, tid, NT);
+    if (G > 1) load_x(xr, x, set_t0(1) / 9, n_boards, chunk_of(1) * KC, tid);
     __syncthreads();
-    store_x(sX, xr, tid);
+    if (G > 1) store_x(sX, xr, tid);
     __syncthreads();
-    // waves w and w+4 share a SIMD: one transforms while the other issues MFMAs
+    // Waves w and w+4 share a SIMD. A chunk's transform is 256 tile-pair items,
+    // one per lane of one wave per SIMD: one half of the workgroup transforms
+    // (then joins the GEMMs) while the other half starts its MFMAs at once; the
+    // halves alternate by chunk so both carry the same delay.
     const int tfirst = tid & 255;
     if ((MODE & 8) && wv >= 4) __builtin_amdgcn_s_setprio(1);
-    // the younger half (waves 4-7) transforms first: the older half, which wins
-    // issue arbitration, starts its MFMAs at once (+2% over the reverse order)
-    const bool tr_first = (MODE & 16) ? wv < 4 : wv >= 4;
+    const int my_half = (wv >= 4) ^ ((MODE & 16) ? 1 : 0);
     const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
     unsigned long long ts = stamp ? __builtin_amdgcn_s_memtime() : 0;
+    int gs = 0;
     auto mark = [&](int k) {
-        if (stamp) {
+        if (stamp && gs < NCH) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
             g_phase[blockIdx.x][tid >> 8][k] = (unsigned int)(t - ts);
             ts = t;
@@ -324,69 +337,91 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
     };
     if (stamp) g_phase[blockIdx.x][tid >> 8][0] = (unsigned int)(ts - t_core);
 #pragma unroll 1
-    for (int c = 0; c < NCH; ++c) {
-        const int ch = (c + c_rot) % NCH;
-        if (c + 2 < NCH) load_x(xr, x, b0, n_boards, ((ch + 2) % NCH) * KC, tid);
-        const bool tr = (MODE & 3) != 1 && c + 1 < NCH;
-        if (tr && tr_first) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
-        if (tr_first) mark(1 + 4 * c);
+    for (int g = 0; g < G; ++g) {
+        gs = g;
+        const int c = g % NCH, ch = chunk_of(g);
+        if (g + 2 < G) load_x(xr, x, set_t0(g + 2) / 9, n_boards, chunk_of(g + 2) * KC, tid);
+        const bool tr = (MODE & 3) != 1 && g + 1 < G && my_half == (g & 1 ? 0 : 1);
+        if (tr) {
+            if (MODE & 128) __builtin_amdgcn_s_setprio(3);
+            transform(sV[(g + 1) & 1], sX, set_t0(g + 1), set_t0(g + 1) / 9, tfirst, 256);
+            if (MODE & 128) __builtin_amdgcn_s_setprio(0);
+        }
+        mark(1 + 4 * c);
         if constexpr ((MODE & 3) != 2) {
-            const floatx2 *sv = reinterpret_cast<const floatx2 *>(sV[c & 1]) + lane;
+            const floatx2 *sv = reinterpret_cast<const floatx2 *>(sV[g & 1]) + lane;
             floatx2 a0[KC / 4], a1[KC / 4];
             load_a(a0, sv, 0);
             load_a(a1, sv, 1);
             floatx2 mprev[4];
             xi_loop<0, MODE>(S, sv, ur, b0v, b1v, b2v, a0, a1, mprev, k2, k4, ch, voff);
         }
+        if (c == NCH - 1) {
+            // epilogue of this set: Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is
+            // tile 16rt + 4(lane>>4) + r, output (3ty+a, 3tx+b); + bias, + residual, ReLU
+            const int t0 = set_t0(g);
+            floatx8 Y[9];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    floatx8 acc = {};
+#pragma unroll
+                    for (int v = 0; v < 5; ++v) {
+                        if (at(b, v) == 0) continue;
+                        const Acc &q = S[a * 5 + v];
+                        const floatx8 sv8 = {q.p[0].x, q.p[0].y, q.p[1].x, q.p[1].y,
+                                             q.p[2].x, q.p[2].y, q.p[3].x, q.p[3].y};
+                        acc = at(b, v) == 1 ? acc + sv8
+                            : at(b, v) == -1 ? acc - sv8
+                                             : __builtin_elementwise_fma(floatx8((float)at(b, v)), sv8, acc);
+                    }
+                    Y[a * 3 + b] = acc;
+                }
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int T = t0 + 16 * rt + 4 * (lane >> 4) + r;
+                    if (T >= ntiles) continue;
+                    const int board = T / 9, tt = T % 9, ty = tt / 3, tx = tt % 3;
+#pragma unroll
+                    for (int ab = 0; ab < 9; ++ab) {
+                        const size_t idx = ((size_t)board * 81 + (3 * ty + ab / 3) * 9 + 3 * tx + ab % 3) * C + co;
+                        float v = Y[ab][4 * rt + r] + bb;
+                        if (RES) v += res[idx];
+                        y[idx] = fmaxf(v, 0.0f);
+                    }
+                }
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+        }
         mark(2 + 4 * c);
-        if (tr && !tr_first) transform(sV[(c + 1) & 1], sX, t0, b0, tfirst, 256);
-        if (!tr_first) mark(1 + 4 * c);
         __syncthreads();
         mark(3 + 4 * c);
-        if (c + 2 < NCH) store_x(sX, xr, tid);
+        if (g + 2 < G) store_x(sX, xr, tid);
         __syncthreads();
         mark(4 + 4 * c);
     }
-
-    // epilogue: Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is tile 16rt + 4(lane>>4) + r,
-    // output (3ty+a, 3tx+b); + bias, + residual, ReLU
-    floatx8 Y[9];
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            floatx8 acc = {};
-#pragma unroll
-            for (int v = 0; v < 5; ++v) {
-                if (at(b, v) == 0) continue;
-                const Acc &q = S[a * 5 + v];
-                const floatx8 sv8 = {q.p[0].x, q.p[0].y, q.p[1].x, q.p[1].y, q.p[2].x, q.p[2].y, q.p[3].x, q.p[3].y};
-                acc = at(b, v) == 1 ? acc + sv8
-                    : at(b, v) == -1 ? acc - sv8
-                                     : __builtin_elementwise_fma(floatx8((float)at(b, v)), sv8, acc);
-            }
-            Y[a * 3 + b] = acc;
-        }
     if ((MODE & 4) && tid == 0 && blockIdx.x < 4096) {
-        g_clk[blockIdx.x][0] = __builtin_amdgcn_s_memtime() - t_core;
-        g_clk[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime() - t_real;
+        g_clk[blockIdx.x][0] = (__builtin_amdgcn_s_memtime() - t_core) / my_sets;
+        g_clk[blockIdx.x][1] = (__builtin_amdgcn_s_memrealtime() - t_real) / my_sets;
     }
-    const float bb = bias[co];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int T = t0 + 16 * rt + 4 * (lane >> 4) + r;
-            if (T >= ntiles) continue;
-            const int board = T / 9, tt = T % 9, ty = tt / 3, tx = tt % 3;
-#pragma unroll
-            for (int ab = 0; ab < 9; ++ab) {
-                const size_t idx = ((size_t)board * 81 + (3 * ty + ab / 3) * 9 + 3 * tx + ab % 3) * C + co;
-                float v = Y[ab][4 * rt + r] + bb;
-                if (RES) v += res[idx];
-                y[idx] = fmaxf(v, 0.0f);
-            }
-        }
+}
+
+// One workgroup per CU (LDS and registers allow exactly one), never more than tile sets.
+static int grid_size(int n_boards) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+    }
+    const int nsets = (n_boards * 9 + WT - 1) / WT;
+    return nsets < cus ? nsets : cus;
 }
 
 }  // namespace wino3
@@ -432,7 +467,7 @@ int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, con
         return UTTT_ERR_ARG;
     }
     if (n_boards == 0) return UTTT_OK;
-    const dim3 grid((n_boards * 9 + wino3::WT - 1) / wino3::WT);
+    const dim3 grid(wino3::grid_size(n_boards));
     if (residual)
         hipLaunchKernelGGL(wino3::k_wino3_conv<true>, grid, dim3(wino3::NT), 0, (hipStream_t)stream, x, u, bias, residual,
                            y, n_boards);
@@ -450,7 +485,7 @@ int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, con
 // Diagnostic (not declared in uttt_nn.h): the same launch with a timing ablation.
 int uttt_diag_wino3_ablation(const float *x, const float *u, const float *bias, float *y, int32_t n_boards,
                              int32_t mode, void *stream) {
-    const dim3 grid((n_boards * 9 + wino3::WT - 1) / wino3::WT);
+    const dim3 grid(wino3::grid_size(n_boards));
     hipStream_t st = (hipStream_t)stream;
     using namespace wino3;
     switch (mode) {
@@ -465,6 +500,10 @@ int uttt_diag_wino3_ablation(const float *x, const float *u, const float *bias, 
         case 24: hipLaunchKernelGGL((k_wino3_conv<false, 24>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 33: hipLaunchKernelGGL((k_wino3_conv<false, 33>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 35: hipLaunchKernelGGL((k_wino3_conv<false, 35>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 128: hipLaunchKernelGGL((k_wino3_conv<false, 128>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 144: hipLaunchKernelGGL((k_wino3_conv<false, 144>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 6: hipLaunchKernelGGL((k_wino3_conv<false, 6>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 69: hipLaunchKernelGGL((k_wino3_conv<false, 69>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 97: hipLaunchKernelGGL((k_wino3_conv<false, 97>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 65: hipLaunchKernelGGL((k_wino3_conv<false, 65>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         default: hipLaunchKernelGGL((k_wino3_conv<false, 0>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards);
