@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
     ap.add_argument("--cudnn-benchmark", type=int, default=1)
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="engines per GPU, each on its own stream; their network evaluations overlap")
     ap.add_argument("--cache-log2", type=int, default=21, help="evaluation cache entries (log2); 0 = off")
     ap.add_argument("--tag", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -181,33 +183,43 @@ def main():
     G, S, B = args.games, args.sims, args.batch
     net = random_network(0, dev)
     model = FoldedDualNetwork(net).to(dev) if args.evaluator == "nn" else net
-    sp = SelfPlay(G, S, B, 1.0, device=local, model=model, cache_log2=args.cache_log2)
+    sp = SelfPlay(G, S, B, 1.0, device=local, cache_log2=args.cache_log2, lanes=args.lanes)
     if args.evaluator == "hash":
-        sp.evaluator = HashEvaluator(sp.engine)
+        make_inner = HashEvaluator
     elif args.evaluator.startswith("fused"):
         conv = {"fused": "wino3", "fused-wino2": "wino", "fused-miopen": "miopen"}[args.evaluator]
-        sp.evaluator = FusedNetworkEvaluator(net, sp.engine, conv=conv)
+        make_inner = lambda eng: FusedNetworkEvaluator(net, eng, conv=conv)  # noqa: E731
+    else:
+        make_inner = lambda eng: NetworkEvaluator(model, eng.max_trees)  # noqa: E731
 
-    # NN timing (events on the stream the evaluator runs on) and useful rows
+    # NN timing: events around every evaluation on the stream it runs on (lanes
+    # overlap, so busy time is the union of the intervals), and useful rows
     nn_stats = {"ms": 0.0, "rows": 0, "padded_rows": 0}
-    inner = sp.evaluator
     ev_pairs = []
+    pads = args.evaluator in ("nn", "nn-plain", "fused-miopen")
 
-    def timed_eval(x, n):
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record()
-        out = inner(x, n)
-        b.record()
-        ev_pairs.append((a, b))
-        nn_stats["rows"] += n
-        if isinstance(inner, (NetworkEvaluator, FusedNetworkEvaluator)):
-            from uttt_amd.selfplay import _bucket
-            nn_stats["padded_rows"] += _bucket(n, G)
-        return out
+    def make_timed(eng):
+        inner = make_inner(eng)
 
-    timed_eval.needs_input = getattr(inner, "needs_input", True)
-    sp.evaluator = timed_eval
+        def timed_eval(x, n):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            out = inner(x, n)
+            b.record()
+            ev_pairs.append((a, b))
+            nn_stats["rows"] += n
+            if pads:
+                from uttt_amd.selfplay import _bucket
+                nn_stats["padded_rows"] += _bucket(n, eng.max_trees)
+            else:
+                nn_stats["padded_rows"] += n
+            return out
+
+        timed_eval.needs_input = getattr(inner, "needs_input", True)
+        return timed_eval
+
+    sp.set_evaluator(make_timed)
     games_per_rank = 10**9
     arena = (args.age + args.warmup + args.steps + 2) * G
     sp.begin(rank * games_per_rank, (rank + 1) * games_per_rank, 1234, arena_plies=arena)
@@ -223,13 +235,15 @@ def main():
     torch.cuda.synchronize()
     ev_pairs.clear()
     nn_stats.update(ms=0.0, rows=0, padded_rows=0)
-    sp.engine.reset_stats()
-    sp.engine.set_timing(True)
+    sp.reset_stats()
+    sp.set_timing(True)
     rounds0, finished0 = sp.rounds, sp.finished
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    base = torch.cuda.Event(enable_timing=True)
+    base.record()
     t0 = time.perf_counter()
     sims = 0
     for _ in range(args.steps):
@@ -240,14 +254,26 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     torch.cuda.synchronize()
-    nn_stats["ms"] = sum(a.elapsed_time(b) for a, b in ev_pairs)
-    sel = sp.engine.kernel_stats("select")
-    app = sp.engine.kernel_stats("apply")
-    enc = sp.engine.kernel_stats("encode")
-    scan = sp.engine.kernel_stats("scan")
-    mend = sp.engine.kernel_stats("move_end")
+    ivs = sorted((base.elapsed_time(a), base.elapsed_time(b)) for a, b in ev_pairs)
+    busy, cur = 0.0, None
+    for lo, hi in ivs:
+        if cur is None or lo > cur[1]:
+            if cur is not None:
+                busy += cur[1] - cur[0]
+            cur = [lo, hi]
+        else:
+            cur[1] = max(cur[1], hi)
+    if cur is not None:
+        busy += cur[1] - cur[0]
+    nn_stats["ms"] = busy
+    nn_stats["sum_ms"] = sum(hi - lo for lo, hi in ivs)
+    sel = sp.kernel_stats("select")
+    app = sp.kernel_stats("apply")
+    enc = sp.kernel_stats("encode")
+    scan = sp.kernel_stats("scan")
+    mend = sp.kernel_stats("move_end")
     rounds = sp.rounds - rounds0
-    cache = sp.engine.cache_stats() if args.cache_log2 else None
+    cache = sp.cache_stats() if args.cache_log2 else None
 
     tot = torch.tensor([float(sims), elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -284,6 +310,7 @@ def main():
                             f"{args.age} moves before warmup); one step = one move of every game",
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
                 "eval_cache_log2": args.cache_log2,
+                "lanes_per_gpu": args.lanes,
                 "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
                                        "Winograd F(3x3,3x3) f32-MFMA HIP kernel (csrc/wino3_conv.hip), stem/heads "
                                        "HIP kernels (csrc/nn_kernels.hip)",
@@ -312,6 +339,7 @@ def main():
             "nn": {
                 "rows_evaluated": nn_stats["rows"], "rows_padded": nn_stats["padded_rows"],
                 "ms": round(nn_stats["ms"], 2), "share_of_step": round(nn_stats["ms"] / 1e3 / elapsed, 4),
+                "lane_sum_ms": round(nn_stats["sum_ms"], 2),
                 "achieved_tflops": round(nn_tflops, 2), "peak_tflops": FP32_PEAK_TFLOPS,
                 "frac": round(nn_tflops / FP32_PEAK_TFLOPS, 4),
                 "flops_basis": "direct-conv equivalent, 2 x MACs of dual_network.py per evaluated row "

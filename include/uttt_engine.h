@@ -96,6 +96,10 @@ int uttt_engine_destroy(uttt_engine_t *eng);
 /* Launch everything on `stream` (a hipStream_t, e.g. torch's current stream;
  * NULL = the null stream). Until called, the engine uses a stream of its own. */
 int uttt_engine_set_stream(uttt_engine_t *eng, void *stream);
+/* The engine's own non-blocking stream (created with the engine; each engine's
+ * stream gets its own hardware queue when few streams exist), e.g. to run an
+ * evaluator on it so that several engines on one GPU overlap. */
+int uttt_engine_own_stream(uttt_engine_t *eng, void **stream);
 /* Device bytes held by the engine. */
 int64_t uttt_engine_device_bytes(const uttt_engine_t *eng);
 

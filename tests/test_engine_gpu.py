@@ -136,16 +136,18 @@ def test_selfplay_matches_reference_driver(gpu):
 
 
 def test_selfplay_matches_oracle_and_is_slot_invariant(gpu, oracle_lib):
+    """Records equal the oracle's for any slot count and any number of lanes
+    (engines on separate streams, round-robined by SelfPlay.step)."""
     core = oracle_lib
     n_games, seed = 24, 777
     ref = [core.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
-    for slots in (1, 7, 32):
-        sp = gpu.SelfPlay(slots, 30, 4, 1.0)
+    for slots, lanes in ((1, 1), (7, 1), (32, 1), (8, 2), (12, 3)):
+        sp = gpu.SelfPlay(slots, 30, 4, 1.0, lanes=lanes)
         sp.run(0, n_games, seed)
         recs = sp.records()
         assert len(recs) == n_games
         for g, r in enumerate(recs):
-            assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (slots, g)
+            assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (slots, lanes, g)
             assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64))
             assert np.array_equal(r["values"], ref[g]["values"].astype(np.int64))
 
@@ -337,6 +339,27 @@ def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib):
     for i, s in enumerate(ostates):
         _, vi, _ = core.pv_mcts_scores(s, 1.0, 50, 8, lambda x: table[np.asarray(x, np.float32).tobytes()])
         assert np.array_equal(visits[i, :L[i]], vi), i
+
+
+def test_fused_selfplay_lanes_are_bit_identical(gpu):
+    """Self-play with the fused network evaluator: 2 lanes (two engines on two
+    streams, network calls overlapping) give the same records bit for bit as one
+    lane - every kernel computes a board independently of the batch it is in."""
+    from uttt_amd.model import random_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    net = random_network(0, "cuda")
+    out = []
+    for lanes in (1, 2):
+        sp = gpu.SelfPlay(16, 50, 8, 1.0, lanes=lanes)
+        sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng))
+        sp.run(0, 12, 4321)
+        out.append(sp.records())
+    a, b = out
+    assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(12))
+    for ra, rb in zip(a, b):
+        assert np.array_equal(ra["actions"], rb["actions"])
+        assert np.array_equal(ra["policies"].view(np.uint64), rb["policies"].view(np.uint64))
+        assert np.array_equal(ra["values"], rb["values"])
 
 
 def test_eval_cache_is_exact(gpu, oracle_lib):

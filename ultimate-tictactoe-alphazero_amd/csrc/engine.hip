@@ -1225,6 +1225,12 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     return UTTT_OK;
 }
 
+int uttt_engine_own_stream(uttt_engine_t *e, void **stream) {
+    if (!e || !stream) return UTTT_ERR_ARG;
+    *stream = (void *)e->own_stream;
+    return UTTT_OK;
+}
+
 int uttt_engine_set_stream(uttt_engine_t *e, void *stream) {
     if (!e) return UTTT_ERR_ARG;
     // NULL is the null (legacy default) stream — what torch.cuda.current_stream()

@@ -57,6 +57,14 @@ class Engine:
         check(self.lib.uttt_engine_set_stream(self.h, ctypes.c_void_p(s.cuda_stream)))
         self.stream = s
 
+    def own_stream(self):
+        """The engine's own non-blocking HIP stream as a torch ExternalStream."""
+        import torch
+
+        p = ctypes.c_void_p()
+        check(self.lib.uttt_engine_own_stream(self.h, ctypes.byref(p)))
+        return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", self.device))
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.uttt_engine_destroy(self.h)

@@ -5,6 +5,8 @@ search whose flushes call the network at batch <= 8 (self_play_cpp.py:104-130,
 pv_mcts_cpp.py:37-87). Here all games of a shard advance together: each round
 every live tree contributes its one pending leaf to a single network batch.
 """
+import collections
+import contextlib
 import math
 import time
 
@@ -83,58 +85,135 @@ class BatchedSearch:
         return self.engine.root_visits()
 
 
+class _Lane:
+    """One engine + its stream, input buffer and evaluator."""
+
+    def __init__(self, slots, evaluate_count, device, cache_log2, cache_clear_every, own_stream):
+        self.engine = Engine(slots, evaluate_count, device)
+        if cache_log2:
+            self.engine.set_cache(cache_log2, cache_clear_every)
+        # lanes run on their engines' own streams: streams created later (e.g. from
+        # torch's pool) can share one of the few hardware queues and serialize
+        self.stream = self.engine.own_stream() if own_stream else None
+        dev = torch.device("cuda", self.engine.device)
+        self.x = torch.zeros((slots, 3, 9, 9), dtype=torch.float32, device=dev)
+        self.evaluator = None
+        self.rounds = 0
+        self.finished = 0
+
+    def use_stream(self):
+        self.engine.use_stream(self.stream)
+
+
 class SelfPlay:
     """Concurrent self-play of games [begin, end) with `slots` trees in flight.
 
     Game g draws its moves from numpy's legacy MT19937 seeded seed_base + g, so
     its record equals self_play_cpp.play after np.random.seed(seed_base + g)
-    (same model), independent of slot count, shard or GPU count."""
+    (same model), independent of slot count, shard or GPU count.
+
+    lanes > 1 splits the slots (and the game range) over that many engines, each
+    on its own HIP stream with its own evaluator. A step round-robins the lanes:
+    while the host waits for one lane's pending count, the other lanes' network
+    evaluations run, and their convolution kernels fill each other's partial
+    last waves on the GPU. Records are unchanged (each game depends only on its id)."""
 
     def __init__(self, slots, evaluate_count=50, batch_size=8, temperature=1.0, device=None, evaluator=None,
-                 model=None, cache_log2=None, cache_clear_every=32):
-        self.engine = Engine(slots, evaluate_count, device)
+                 model=None, cache_log2=None, cache_clear_every=32, lanes=1):
+        if lanes < 1 or slots % lanes:
+            raise ValueError("slots must be a positive multiple of lanes")
+        per = slots // lanes
         if cache_log2 is None:  # ~512 entries per slot: a 32-move window of one game's leaves
-            cache_log2 = min(21, max(12, int(math.ceil(math.log2(max(slots, 1)))) + 9))
-        if cache_log2:
-            self.engine.set_cache(cache_log2, cache_clear_every)
+            cache_log2 = min(21, max(12, int(math.ceil(math.log2(max(per, 1)))) + 9))
+        self.lanes = []
+        for i in range(lanes):
+            self.lanes.append(_Lane(per, evaluate_count, device, cache_log2, cache_clear_every, lanes > 1))
+        self.engine = self.lanes[0].engine
+        self.x = self.lanes[0].x
         self.slots = slots
         self.evaluate_count = evaluate_count
         self.batch_size = batch_size
         self.temperature = temperature
-        dev = torch.device("cuda", self.engine.device)
-        self.x = torch.zeros((slots, 3, 9, 9), dtype=torch.float32, device=dev)
-        if evaluator is None:
-            evaluator = HashEvaluator(self.engine) if model is None else NetworkEvaluator(model, slots)
-        self.evaluator = evaluator
+        if evaluator is None and model is not None:
+            self.set_evaluator(lambda eng: NetworkEvaluator(model, eng.max_trees))
+        elif evaluator is None:
+            self.set_evaluator(HashEvaluator)
+        else:
+            self.evaluator = evaluator
         self.sims = 0
-        self.rounds = 0
         self.moves = 0
-        self.finished = 0
+
+    # one evaluator object per lane (each owns its buffers); with one lane the
+    # attribute form is kept for compatibility
+    def set_evaluator(self, make):
+        """make(engine) -> evaluator, called once per lane."""
+        for ln in self.lanes:
+            ln.evaluator = make(ln.engine)
+
+    @property
+    def evaluator(self):
+        return self.lanes[0].evaluator
+
+    @evaluator.setter
+    def evaluator(self, ev):
+        if len(self.lanes) > 1:
+            raise ValueError("with lanes > 1 use set_evaluator(make) (one evaluator per lane)")
+        self.lanes[0].evaluator = ev
+
+    @property
+    def rounds(self):
+        return sum(ln.rounds for ln in self.lanes)
+
+    @property
+    def finished(self):
+        return sum(ln.finished for ln in self.lanes)
+
+    def _ctx(self, ln):
+        return torch.cuda.stream(ln.stream) if ln.stream is not None else contextlib.nullcontext()
 
     def begin(self, game_begin, game_end, seed_base, arena_plies=None):
-        self.engine.use_stream()
-        self.engine.selfplay_begin(game_begin, game_end, seed_base, self.temperature, self.evaluate_count,
-                                   self.batch_size, arena_plies)
-        self.sims = self.rounds = self.moves = 0
-        self.finished = 0
+        n = len(self.lanes)
+        span = game_end - game_begin
+        for i, ln in enumerate(self.lanes):
+            gb = game_begin + span * i // n
+            ge = game_begin + span * (i + 1) // n
+            if ln.stream is None:
+                ln.engine.use_stream()
+            else:
+                ln.use_stream()
+            with self._ctx(ln):
+                ln.engine.selfplay_begin(gb, ge, seed_base, self.temperature, self.evaluate_count, self.batch_size,
+                                         arena_plies if arena_plies is None else -(-arena_plies // n))
+            ln.rounds = ln.finished = 0
+        self.sims = self.moves = 0
 
     def step(self):
         """One move for every live game. Returns the simulations it ran (0 = all games over)."""
-        e = self.engine
-        live = e.move_begin()
-        if live == 0:
+        live = []
+        for ln in self.lanes:
+            with self._ctx(ln):
+                live.append(ln.engine.move_begin())
+        active = [ln for ln, n in zip(self.lanes, live) if n > 0]
+        if not active:
             return 0
-        x = self.x if getattr(self.evaluator, "needs_input", True) else None
-        while True:
-            n = e.select(x)
-            if n == 0:
-                break
-            p, v = self.evaluator(self.x, n)
-            e.apply(p, v)
-            self.rounds += 1
-        self.finished = e.move_end()
+        queue = collections.deque(active)
+        while queue:
+            ln = queue.popleft()
+            e = ln.engine
+            with self._ctx(ln):
+                x = ln.x if getattr(ln.evaluator, "needs_input", True) else None
+                n = e.select(x)  # waits for this lane's previous round only
+                if n == 0:
+                    continue
+                p, v = ln.evaluator(ln.x, n)
+                e.apply(p, v)
+                ln.rounds += 1
+            queue.append(ln)
+        for ln in active:
+            with self._ctx(ln):
+                ln.finished = ln.engine.move_end()
         self.moves += 1
-        done = live * self.evaluate_count
+        done = sum(live) * self.evaluate_count
         self.sims += done
         return done
 
@@ -146,18 +225,44 @@ class SelfPlay:
                 progress(self.finished, game_end - game_begin)
         return time.time() - t0
 
+    def kernel_stats(self, name):
+        out = {"ms": 0.0, "launches": 0, "bytes": 0}
+        for ln in self.lanes:
+            st = ln.engine.kernel_stats(name)
+            for k in out:
+                out[k] += st[k]
+        return out
+
+    def cache_stats(self):
+        out = {"hits": 0, "misses": 0, "inserts": 0}
+        for ln in self.lanes:
+            st = ln.engine.cache_stats()
+            for k in out:
+                out[k] += st[k]
+        return out
+
+    def set_timing(self, on=True):
+        for ln in self.lanes:
+            ln.engine.set_timing(on)
+
+    def reset_stats(self):
+        for ln in self.lanes:
+            ln.engine.reset_stats()
+
     def records(self, with_inputs=True):
         """Finished games sorted by id: dict of per-game lists."""
-        ids, off, ln = self.engine.games()
-        pl = self.engine.plies(with_inputs)
         out = []
-        for g, o, n in zip(ids.tolist(), off.tolist(), ln.tolist()):
-            rec = {"game": g, "actions": pl["actions"][o:o + n].astype(np.int64),
-                   "policies": pl["policies"][o:o + n], "values": pl["values"][o:o + n].astype(np.int64),
-                   "states": pl["states"][o:o + n]}
-            if with_inputs:
-                rec["inputs"] = pl["inputs_hwc"][o:o + n].reshape(n, 9, 9, 3)
-            out.append(rec)
+        for ln in self.lanes:
+            ids, off, ln_ = ln.engine.games()
+            pl = ln.engine.plies(with_inputs)
+            for g, o, n in zip(ids.tolist(), off.tolist(), ln_.tolist()):
+                rec = {"game": g, "actions": pl["actions"][o:o + n].astype(np.int64),
+                       "policies": pl["policies"][o:o + n], "values": pl["values"][o:o + n].astype(np.int64),
+                       "states": pl["states"][o:o + n]}
+                if with_inputs:
+                    rec["inputs"] = pl["inputs_hwc"][o:o + n].reshape(n, 9, 9, 3)
+                out.append(rec)
+        out.sort(key=lambda r: r["game"])
         return out
 
 
