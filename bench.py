@@ -29,6 +29,21 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 (vector = matrix) peak
 
 
+def select_traffic(trees_per_launch):
+    """HBM bytes per k_select launch from the committed PMC summary (tools/pmc_select.sh ->
+    tools/pmc_summary.py; FETCH_SIZE + WRITE_SIZE, separate passes, raw - see that file),
+    when it was taken at this launch size; else None. A live bench run cannot read PMC."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_select.json")), reverse=True):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("trees_per_launch") == trees_per_launch:
+            return {"bytes_per_launch": round(d["traffic_bytes_raw"]),
+                    "read_bytes": round(d["fetch_bytes"]), "write_bytes": round(d["write_bytes"]),
+                    "source": os.path.relpath(f, REPO)}
+    return None
+
+
 def nn_macs():
     f, k, r = 128, 9, 81
     macs = r * f * 3 * k + 32 * r * f * f * k          # stem + 16 blocks x 2 convs
@@ -331,7 +346,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": (select_traffic(G // args.lanes) or {}).get("bytes_per_launch"),
+                "traffic_detail": select_traffic(G // args.lanes),
                 "algo_bytes_per_launch": round(sel["bytes"] / max(sel["launches"], 1)),
                 "avg_launch_us": round(sel_ms * 1e3 / max(sel["launches"], 1), 2),
                 "launches": sel["launches"],
