@@ -171,6 +171,11 @@ int uttt_selfplay_plies(uttt_engine_t *eng, uttt_state_t *states, double *polici
                         int8_t *values, float *inputs_hwc, int64_t max_plies, int64_t *n_plies);
 
 /* ----------------------------------------------------- evaluation cache --- */
+/* Use `owner`'s evaluation table instead of a private one (several engines on
+ * one GPU, e.g. SelfPlay lanes, then see each other's evaluations). Lookups and
+ * inserts are coherent across concurrently running kernels; only the owner
+ * clears the table (its clear_every_moves). The owner must outlive `eng`. */
+int uttt_engine_share_cache(uttt_engine_t *eng, uttt_engine_t *owner);
 /* Position -> raw evaluator output table in HBM (2^log2_capacity entries of
  * 360 B; 0 = off, the default). A flushed leaf whose position is cached is
  * expanded from the table inside the select kernel instead of waiting for the

@@ -176,28 +176,66 @@ __device__ __forceinline__ bool same_state(const uttt_state_t &x, const uttt_sta
            x.opp[1] == y.opp[1] && x.opp[2] == y.opp[2] && x.mains == y.mains && x.active == y.active;
 }
 
+// The table may be shared by several engines whose kernels run concurrently on
+// other XCDs, whose L2s are not coherent with this one: every access to flag,
+// key and val is an agent-scope atomic (sc1: served from memory, not from a
+// possibly stale L2 line). Entries are exact (the evaluator is a pure function
+// of the position), so any ready entry with a matching key is correct; a
+// reader re-checks flag and key after copying the values so an entry recycled
+// meanwhile (clear + re-insert) is never mixed into the copy.
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool key_is(const EvalCache &c, uint32_t slot, const uttt_state_t &s) {
+    const uint32_t *k = reinterpret_cast<const uint32_t *>(c.key + slot);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&s);
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) same &= ld_agent(k + i) == w[i];
+    return same;
+}
+
 // Wave-uniform lookup, the kProbe slots probed by lanes 0..kProbe-1 at once:
-// a hit counts only if no empty slot precedes it in probe order.
-__device__ __forceinline__ int cache_find(const EvalCache &c, const uttt_state_t &s) {
-    if (!c.flag) return -1;
+// a hit counts only if no empty slot precedes it in probe order. On a hit the
+// 82 values are copied to dst (LDS) and true is returned.
+__device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *dst) {
+    if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
-    const uint32_t slot = (state_hash(s) + (uint32_t)lane) & c.mask;
+    const uint32_t h = state_hash(s);
+    const uint32_t slot = (h + (uint32_t)lane) & c.mask;
     uint32_t f = 0u;
     bool same = false;
     if (lane < kProbe) {
-        f = c.flag[slot];
-        if (f == 2u) same = same_state(c.key[slot], s);
+        f = ld_agent(c.flag + slot);
+        if (f == 2u) same = key_is(c, slot, s);
     }
     const uint64_t hit = __ballot(lane < kProbe && f == 2u && same);
     const uint64_t empty = __ballot(lane < kProbe && f == 0u);
-    if (!hit) return -1;
+    if (!hit) return false;
     const int hl = __builtin_ctzll(hit);
-    if (empty && __builtin_ctzll(empty) < hl) return -1;
-    return __builtin_amdgcn_readfirstlane((int)((state_hash(s) + (uint32_t)hl) & c.mask));
+    if (empty && __builtin_ctzll(empty) < hl) return false;
+    const uint32_t hs = (h + (uint32_t)hl) & c.mask;
+    const float *src = c.val + (size_t)hs * kCacheVal;
+    const float v0 = ld_agent(src + lane);
+    const float v1 = lane < kCacheVal - 64 ? ld_agent(src + 64 + lane) : 0.0f;
+    bool ok = true;
+    if (lane == 0) ok = ld_agent(c.flag + hs) == 2u && key_is(c, hs, s);
+    if (!__shfl(ok, 0)) return false;
+    dst[lane] = v0;
+    if (lane < kCacheVal - 64) dst[64 + lane] = v1;
+    return true;
 }
 
-// Wave-level insert of (s -> pol[0..80], v). Lane 0 claims a slot by CAS;
-// a concurrent insert of the same key may leave a harmless duplicate.
+// Wave-level insert of (s -> pol[0..80], v). Lane 0 claims a slot by CAS; the
+// payload is stored at agent scope and drained (s_waitcnt vmcnt(0)) before the
+// flag is published, so a reader on any XCD that sees the flag sees the data.
+// A concurrent insert of the same key may leave a harmless duplicate.
 __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const float *pol, float v) {
     if (!c.flag) return;
     const int lane = (int)(threadIdx.x & 63);
@@ -206,8 +244,8 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
         const uint32_t h = state_hash(s);
         for (int i = 0; i < kProbe; ++i) {
             const uint32_t sl = (h + (uint32_t)i) & c.mask;
-            const uint32_t f = __hip_atomic_load(c.flag + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (f == 2u && same_state(c.key[sl], s)) break;
+            const uint32_t f = ld_agent(c.flag + sl);
+            if (f == 2u && key_is(c, sl, s)) break;
             if (f == 0u && atomicCAS(c.flag + sl, 0u, 1u) == 0u) {
                 slot = (int)sl;
                 break;
@@ -217,13 +255,13 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
     slot = __shfl(slot, 0);
     if (slot < 0) return;
     float *dst = c.val + (size_t)slot * kCacheVal;
-    dst[lane] = pol[lane];
-    if (lane < 17) dst[64 + lane] = pol[64 + lane];
-    if (lane == 17) dst[81] = v;
-    if (lane == 0) c.key[slot] = s;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    st_agent(dst + lane, pol[lane]);
+    if (lane < 17) st_agent(dst + 64 + lane, pol[64 + lane]);
+    if (lane == 17) st_agent(dst + 81, v);
+    if (lane < 8) st_agent(reinterpret_cast<uint32_t *>(c.key + slot) + lane, reinterpret_cast<const uint32_t *>(&s)[lane]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
-        __hip_atomic_store(c.flag + slot, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_agent(c.flag + slot, 2u);
         atomicAdd(c.ctr + 2, 1ull);
     }
 }
@@ -348,6 +386,7 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 // accounted by k.
 __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCache cache,
                                                    unsigned long long *bytes_ctr) {
+    __shared__ float s_hit[kWavesPerBlock][kCacheVal];  // a cache hit's values, per wave
     const int lane = lane_id();
     const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (t >= tr.n_trees) return;
@@ -437,9 +476,8 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
             // Unexpanded leaf (n == 0 && no children, uttt_mcts.cpp:121): queue it with
             // k = the copies the reference would queue before flushing (:127).
             const int k = min(tr.batch, tr.sims - sims_done);
-            const int hit = cache_find(cache, s);
-            if (hit >= 0) {  // the flush's evaluation is already known: apply it now
-                const float *cv = cache.val + (size_t)hit * kCacheVal;
+            float *cv = s_hit[threadIdx.x >> 6];
+            if (cache_lookup(cache, s, cv)) {  // the flush's evaluation is already known: apply it now
                 if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
@@ -1013,6 +1051,7 @@ struct uttt_engine {
     EvalCache cache{};
     int cache_log2 = 0;
     int cache_clear_every = 0;
+    bool cache_owner = true;  // false: the table belongs to another engine (uttt_engine_share_cache)
     int64_t moves = 0;
     unsigned long long *d_cache_ctr = nullptr;
     // telemetry
@@ -1216,9 +1255,11 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     if (e->d_pol_scratch) (void)hipFree(e->d_pol_scratch);
     if (e->d_val_scratch) (void)hipFree(e->d_val_scratch);
     if (e->d_rowbase) (void)hipFree(e->d_rowbase);
-    if (e->cache.flag) (void)hipFree(e->cache.flag);
-    if (e->cache.key) (void)hipFree(e->cache.key);
-    if (e->cache.val) (void)hipFree(e->cache.val);
+    if (e->cache_owner) {
+        if (e->cache.flag) (void)hipFree(e->cache.flag);
+        if (e->cache.key) (void)hipFree(e->cache.key);
+        if (e->cache.val) (void)hipFree(e->cache.val);
+    }
     if (e->h_count) (void)hipHostFree(e->h_count);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -1647,7 +1688,7 @@ int uttt_engine_set_cache(uttt_engine_t *e, int32_t log2_capacity, int32_t clear
     }
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (e->cache.flag) {
+    if (e->cache.flag && e->cache_owner) {
         (void)hipFree(e->cache.flag);
         (void)hipFree(e->cache.key);
         (void)hipFree(e->cache.val);
@@ -1655,6 +1696,7 @@ int uttt_engine_set_cache(uttt_engine_t *e, int32_t log2_capacity, int32_t clear
                               << e->cache_log2);
     }
     e->cache = EvalCache{};
+    e->cache_owner = true;
     e->cache_log2 = log2_capacity;
     e->cache_clear_every = clear_every_moves;
     if (log2_capacity == 0) return UTTT_OK;
@@ -1668,9 +1710,24 @@ int uttt_engine_set_cache(uttt_engine_t *e, int32_t log2_capacity, int32_t clear
     return uttt_engine_cache_clear(e);
 }
 
+int uttt_engine_share_cache(uttt_engine_t *e, uttt_engine_t *owner) {
+    if (!e || !owner || e == owner || !owner->cache_owner || e->device != owner->device) {
+        set_error("uttt_engine_share_cache: need a distinct owner engine (with its own table) on the same device");
+        return UTTT_ERR_ARG;
+    }
+    int rc = uttt_engine_set_cache(e, 0, 0);  // drop this engine's own table
+    if (rc) return rc;
+    e->cache = owner->cache;
+    e->cache.ctr = e->d_cache_ctr;  // statistics stay per engine
+    e->cache_log2 = owner->cache_log2;
+    e->cache_clear_every = 0;       // only the owner clears
+    e->cache_owner = false;
+    return UTTT_OK;
+}
+
 int uttt_engine_cache_clear(uttt_engine_t *e) {
     if (!e) return UTTT_ERR_ARG;
-    if (!e->cache.flag) return UTTT_OK;
+    if (!e->cache.flag || !e->cache_owner) return UTTT_OK;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemsetAsync(e->cache.flag, 0, sizeof(uint32_t) * ((size_t)1 << e->cache_log2), e->stream));
     return UTTT_OK;

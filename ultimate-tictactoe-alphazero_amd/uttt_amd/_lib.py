@@ -58,6 +58,7 @@ SIGNATURES = {
     "uttt_boltzman": (ctypes.c_int, [_F32P, _I32, _F32, _F32P]),
     "uttt_engine_create": (ctypes.c_int, [_I32, _I32, _I32, ctypes.POINTER(_P)]),
     "uttt_engine_destroy": (ctypes.c_int, [_P]),
+    "uttt_engine_share_cache": (ctypes.c_int, [_P, _P]),
     "uttt_engine_own_stream": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     "uttt_engine_set_stream": (ctypes.c_int, [_P, _P]),
     "uttt_engine_device_bytes": (ctypes.c_int64, [_P]),

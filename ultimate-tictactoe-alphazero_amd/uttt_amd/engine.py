@@ -194,6 +194,11 @@ class Engine:
         """Position -> evaluation table in HBM (0 = off). Exact for a deterministic evaluator."""
         check(self.lib.uttt_engine_set_cache(self.h, int(log2_capacity), int(clear_every_moves)))
 
+    def share_cache(self, owner):
+        """Use owner's evaluation table (engines on the same GPU); owner must outlive self."""
+        check(self.lib.uttt_engine_share_cache(self.h, owner.h))
+        self._cache_owner = owner  # keep the table's owner alive
+
     def cache_clear(self):
         check(self.lib.uttt_engine_cache_clear(self.h))
 

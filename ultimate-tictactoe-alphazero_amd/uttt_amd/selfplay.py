@@ -127,7 +127,10 @@ class SelfPlay:
             cache_log2 = min(21, max(12, int(math.ceil(math.log2(max(per, 1)))) + 9))
         self.lanes = []
         for i in range(lanes):
-            self.lanes.append(_Lane(per, evaluate_count, device, cache_log2, cache_clear_every, lanes > 1))
+            self.lanes.append(_Lane(per, evaluate_count, device, cache_log2 if i == 0 else 0, cache_clear_every,
+                                    lanes > 1))
+            if i and cache_log2:  # one table for all lanes: games in different lanes share positions
+                self.lanes[i].engine.share_cache(self.lanes[0].engine)
         self.engine = self.lanes[0].engine
         self.x = self.lanes[0].x
         self.slots = slots
