@@ -17,7 +17,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 x = torch.relu(torch.randn(n, 81, 128)).cuda(); y = torch.empty_like(x)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 names = {0: "full", 1: "no-transform", 2: "no-gemm", 3: "no-fold"}
-names3 = {**names, 16: "swap-roles", 65: "no-transform no-fold", 128: "prio-transform", 144: "prio-transform swapped"}
+names3 = {**names, 65: "no-transform no-fold", 512: "unpinned MFMAs"}
 wc = w.cuda().contiguous(memory_format=torch.channels_last)
 xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
 cases = {}

@@ -92,6 +92,40 @@ __device__ __forceinline__ void fold_xi(Acc (&S)[15], const floatx2 (&m)[4], flo
     fold<at(2, u)>(S[2 * 5 + v], m, k2, k4);
 }
 
+// The fold of a point, as a list of single packed ops: op o = (a, pair j) over the
+// rows a with A^T[a][u] != 0; spread over the next point's 8 MFMAs (an op or two
+// after each) instead of issued in one burst.
+__host__ __device__ constexpr int n_rows(int u) { return (at(0, u) != 0) + (at(1, u) != 0) + (at(2, u) != 0); }
+__host__ __device__ constexpr int nth_row(int u, int i) {
+    int a = 0;
+    for (; a < 3; ++a)
+        if (at(a, u) != 0 && i-- == 0) break;
+    return a;
+}
+
+template <int P, int O>
+__device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    constexpr int u = P / 5, v = P % 5;
+    if constexpr (O < 4 * n_rows(u)) {
+        constexpr int a = nth_row(u, O / 4), j = O % 4, K = at(a, u);
+        if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        else if constexpr (K == -1)
+            asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        else if constexpr (K == 2) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k2));
+        else asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k4));
+    }
+}
+
+// ops of point P that go after MFMA slot SL (0..7)
+template <int P, int SL, int O = 0>
+__device__ __forceinline__ void fold_slot(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    constexpr int nops = 4 * n_rows(P / 5);
+    if constexpr (O < nops) {
+        if constexpr (O * 8 / nops == SL) fold_op<P, O>(S, m, k2, k4);
+        fold_slot<P, SL, O + 1>(S, m, k2, k4);
+    }
+}
+
 // U stored in B-fragment order U[xi][chunk][co][q][ks] (ci = chunk*16 + 4ks + q):
 // a lane's 4 values of one point are 16 contiguous bytes.
 __device__ __forceinline__ floatx4 load_b(rsrc_t u, int xi, int chunk, int voff) {
@@ -136,11 +170,19 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const floatx2 *__restrict_
             }
             __builtin_amdgcn_sched_barrier(0);  // keep the prefetches at the top (the scheduler sinks them to their use)
             floatx4 m0 = {}, m1 = {};
-#pragma unroll
-            for (int ks = 0; ks < KC / 4; ++ks) {
-                m0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].x, b0[ks], m0, 0, 0, 0);
-                m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].y, b0[ks], m1, 0, 0, 0);
-            }
+            constexpr bool fold_here = XI > 0 && !(MODE & 64) && (MODE & 3) != 3;
+#define UTTT_SLOT(ks)                                                                   \
+    m0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].x, b0[ks], m0, 0, 0, 0);           \
+    if constexpr (fold_here) fold_slot<XI - 1, 2 * ks>(S, mprev, k2, k4);               \
+    m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks].y, b0[ks], m1, 0, 0, 0);           \
+    if constexpr (fold_here) fold_slot<XI - 1, 2 * ks + 1>(S, mprev, k2, k4);
+            UTTT_SLOT(0) UTTT_SLOT(1) UTTT_SLOT(2) UTTT_SLOT(3)
+#undef UTTT_SLOT
+            static_assert(KC / 4 == 4, "slot sequence written for four k-steps");
+            // pin this point's MFMAs inside its own region (a use here), so the
+            // previous point's fold issues among them instead of the MFMAs sinking
+            // to just before their own fold and that fold waiting on the chain
+            if constexpr (!(MODE & 512)) asm volatile("" : "+v"(m0), "+v"(m1));
             m[0] = __builtin_shufflevector(m0, m0, 0, 1);
             m[1] = __builtin_shufflevector(m0, m0, 2, 3);
             m[2] = __builtin_shufflevector(m1, m1, 0, 1);
@@ -156,9 +198,10 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const floatx2 *__restrict_
         }
         if constexpr (XI > 0 && (MODE & 64)) {
             asm volatile("" : "+v"(mprev[0]), "+v"(mprev[1]), "+v"(mprev[2]), "+v"(mprev[3]));  // diagnostic: no fold
-        } else if constexpr (XI > 0) {
-            if constexpr ((MODE & 3) == 3) fold<1>(S[0], mprev, k2, k4);
-            else fold_xi<XI - 1>(S, mprev, k2, k4);
+        } else if constexpr (XI > 0 && (MODE & 3) == 3) {
+            fold<1>(S[0], mprev, k2, k4);
+        } else if constexpr (XI == NP) {
+            fold_xi<XI - 1>(S, mprev, k2, k4);  // the last point: no MFMAs left to spread it over
         }
         if constexpr (XI < NP) {
 #pragma unroll
@@ -503,6 +546,7 @@ int uttt_diag_wino3_ablation(const float *x, const float *u, const float *bias, 
         case 128: hipLaunchKernelGGL((k_wino3_conv<false, 128>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 144: hipLaunchKernelGGL((k_wino3_conv<false, 144>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 6: hipLaunchKernelGGL((k_wino3_conv<false, 6>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
+        case 512: hipLaunchKernelGGL((k_wino3_conv<false, 512>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 69: hipLaunchKernelGGL((k_wino3_conv<false, 69>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 97: hipLaunchKernelGGL((k_wino3_conv<false, 97>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
         case 65: hipLaunchKernelGGL((k_wino3_conv<false, 65>), grid, dim3(NT), 0, st, x, u, bias, nullptr, y, n_boards); break;
