@@ -134,6 +134,14 @@ def lib():
         L.or_pv_mcts_scores_hash.argtypes = [sp, ctypes.c_float, ctypes.c_int, ctypes.c_int, F32P, I32P,
                                              ctypes.POINTER(SearchStats)]
         L.or_boltzman.argtypes = [F32P, ctypes.c_int, ctypes.c_float, F32P]
+        L.or_pv_mcts_scores_py.argtypes = [sp, ctypes.c_double, ctypes.c_int, ctypes.c_int, EVAL_FN,
+                                           ctypes.c_void_p, F64P, I32P, ctypes.POINTER(SearchStats)]
+        L.or_pv_mcts_scores_py_hash.argtypes = [sp, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                                F64P, I32P, ctypes.POINTER(SearchStats)]
+        L.or_evaluate_play_hash.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_uint64, ctypes.c_uint64, I32P, I32P]
+        L.or_np_pairwise_sum_f32.argtypes = [F32P, ctypes.c_int64]
+        L.or_np_pairwise_sum_f32.restype = ctypes.c_float
         L.or_mt_seed.argtypes = [ctypes.POINTER(MT), ctypes.c_uint32]
         L.or_mt_next32.argtypes = [ctypes.POINTER(MT)]
         L.or_mt_next32.restype = ctypes.c_uint32
@@ -187,6 +195,39 @@ def pv_mcts_scores(state, temperature, evaluate_count, batch_size, evaluator):
     n = lib().or_pv_mcts_scores(ctypes.byref(state), float(temperature), int(evaluate_count), int(batch_size),
                                 fn, None, sc.ctypes.data_as(F32P), vi.ctypes.data_as(I32P), ctypes.byref(st))
     return sc[:n].copy(), vi[:n].copy(), st
+
+
+def pv_mcts_scores_py_hash(state, temperature, evaluate_count=50, batch_size=8, salt=0):
+    """pv_mcts.py (Python semantics) with the (salted) hash evaluator -> (scores f64, visits i32, stats).
+    scores is None where the reference raises ZeroDivisionError (no root child visited)."""
+    sc = np.zeros(81, np.float64)
+    vi = np.zeros(81, np.int32)
+    st = SearchStats()
+    n = lib().or_pv_mcts_scores_py_hash(ctypes.byref(state), float(temperature), int(evaluate_count),
+                                        int(batch_size), ctypes.c_uint64(salt), sc.ctypes.data_as(F64P),
+                                        vi.ctypes.data_as(I32P), ctypes.byref(st))
+    vis = vi[:n].copy()
+    if temperature != 0 and vis.sum() == 0:
+        return None, vis, st
+    return sc[:n].copy(), vis, st
+
+
+def evaluate_play_hash(seed, salt_first, salt_second, temperature=1.0, evaluate_count=50, batch_size=8):
+    """evaluate_network.play after np.random.seed(seed), first player = hash(salt_first).
+    Returns (first player's point 0 / 0.5 / 1, actions)."""
+    acts = np.zeros(81, np.int32)
+    na = ctypes.c_int32()
+    r = lib().or_evaluate_play_hash(ctypes.c_uint32(seed), float(temperature), int(evaluate_count), int(batch_size),
+                                    ctypes.c_uint64(salt_first), ctypes.c_uint64(salt_second),
+                                    acts.ctypes.data_as(I32P), ctypes.byref(na))
+    if r < 0:
+        raise RuntimeError("or_evaluate_play_hash: scores / legal length mismatch")
+    return r / 2.0, acts[:na.value].copy()
+
+
+def np_pairwise_sum_f32(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return np.float32(lib().or_np_pairwise_sum_f32(a.ctypes.data_as(F32P), a.size))
 
 
 def boltzman(xs, temperature):

@@ -23,7 +23,8 @@ def mix64(z):
     return z ^ (z >> 31)
 
 
-def hash_eval_np(x):
+def hash_eval_np(x, salt=0):
+    """salt != 0: a different deterministic player (h = mix64(h ^ salt))."""
     x = np.asarray(x, dtype=np.float32).reshape(243)
     w = [0, 0, 0, 0]
     for j in np.nonzero(x != 0.0)[0].tolist():
@@ -31,6 +32,8 @@ def hash_eval_np(x):
     h = GOLD
     for i in range(4):
         h = mix64(h ^ w[i])
+    if salt:
+        h = mix64(h ^ salt)
     mode = (h >> 8) & 15
     pol = np.zeros(81, np.float32)
     scale = np.float32(1.0 / 16777216.0)
@@ -50,7 +53,7 @@ def hash_eval_np(x):
     return pol, np.float32(val)
 
 
-def make_hash_model():
+def make_hash_model(salt=0):
     import torch
 
     class HashModel(torch.nn.Module):
@@ -61,7 +64,7 @@ def make_hash_model():
             pols = np.zeros((xs.shape[0], 81), np.float32)
             vals = np.zeros((xs.shape[0], 1), np.float32)
             for i in range(xs.shape[0]):
-                pols[i], vals[i, 0] = hash_eval_np(xs[i])
+                pols[i], vals[i, 0] = hash_eval_np(xs[i], salt)
             return torch.from_numpy(pols).to(x.device), torch.from_numpy(vals).to(x.device)
 
     return HashModel()

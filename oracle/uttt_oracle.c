@@ -171,12 +171,14 @@ static uint64_t or_mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-void or_hash_eval(const float *x, float *policy, float *value) {
+/* salt != 0 gives a different deterministic player: h = mix64(h ^ salt) */
+void or_hash_eval_salted(const float *x, float *policy, float *value, uint64_t salt) {
     uint64_t w[4] = {0, 0, 0, 0};
     for (int j = 0; j < 243; ++j)
         if (x[j] != 0.0f) w[j >> 6] |= 1ULL << (j & 63);
     uint64_t h = 0x9E3779B97F4A7C15ULL;
     for (int i = 0; i < 4; ++i) h = or_mix64(h ^ w[i]);
+    if (salt) h = or_mix64(h ^ salt);
     uint32_t mode = (uint32_t)((h >> 8) & 15u);
     for (int a = 0; a < 81; ++a) {
         uint64_t r = or_mix64(h + (uint64_t)(a + 1) * 0x9E3779B97F4A7C15ULL);
@@ -189,6 +191,8 @@ void or_hash_eval(const float *x, float *policy, float *value) {
     uint64_t rv = or_mix64(h ^ 0xD6E8FEB86659FD93ULL);
     *value = (float)((int32_t)(rv % 2001ULL) - 1000) / 1000.0f;
 }
+
+void or_hash_eval(const float *x, float *policy, float *value) { or_hash_eval_salted(x, policy, value, 0ULL); }
 
 /* ------------------------------------------------------------------------- */
 /* PV-MCTS (cpp/uttt_mcts.cpp)                                                */
@@ -543,6 +547,276 @@ int or_self_play_game_hash(uint32_t seed, float temperature, int evaluate_count,
                            int32_t *actions_out, int32_t *values_out) {
     return or_self_play_game(seed, temperature, evaluate_count, batch_size, or_eval_hash_cb, NULL,
                              max_plies, tensors_out, policies_out, actions_out, values_out);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Python PV-MCTS (pv_mcts.py) — the arena path (evaluate_network.py).        */
+/* SURVEY Appendix B. Scalar arithmetic follows NumPy 2 promotion (NEP 50:    */
+/* Python scalars are "weak"), the numpy of this image and of the fixtures:   */
+/*  * priors: policy[legal] (f32) / np.sum (f32 pairwise) (pv_mcts.py:46-56); */
+/*    all-zero -> np.ones(float)/L, i.e. float64 priors for that expansion;   */
+/*  * w is an int until the first network value (np.float32) is added;        */
+/*  * PUCT (:120-130): f32 ops with sqrt(t) in double, or float64 where the   */
+/*    prior is float64; np.argmax = first maximum (a NaN counts as maximum);  */
+/*  * root not pre-expanded, expand REPLACES the children (:104-108), queue   */
+/*    test n == 0 (:150); boltzman in Python floats (:190-192).               */
+/* ------------------------------------------------------------------------- */
+typedef struct or_pnode {
+    or_state s;
+    float p;          /* prior (f32) unless p64 */
+    int p64;          /* prior is the float64 uniform 1/nsib */
+    int nsib;         /* |legal| of the parent (for p64) */
+    float w;          /* exact for int-typed w too (|w| small) */
+    int w_f32;        /* w has become np.float32 */
+    int n;
+    struct or_pnode **ch;
+    int nch;          /* -1: child_nodes is None */
+} or_pnode;
+
+static or_pnode *or_pnode_new(const or_state *s) {
+    or_pnode *n = (or_pnode *)calloc(1, sizeof(or_pnode));
+    n->s = *s;
+    n->nch = -1;
+    return n;
+}
+
+static void or_pnode_free(or_pnode *n) {
+    for (int i = 0; i < n->nch; ++i) or_pnode_free(n->ch[i]);
+    free(n->ch);
+    free(n);
+}
+
+/* np.add.reduce over a contiguous float32 array (pairwise, float32 accumulators) */
+float or_np_pairwise_sum_f32(const float *a, int64_t n) {
+    if (n < 8) {
+        float r = 0.0f;
+        for (int64_t i = 0; i < n; ++i) r += a[i];
+        return r;
+    } else if (n <= 128) {
+        float r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int64_t i;
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    } else {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        return or_np_pairwise_sum_f32(a, n2) + or_np_pairwise_sum_f32(a + n2, n - n2);
+    }
+}
+
+/* predict_batch's per-state post-processing (pv_mcts.py:46-56) + expand (:104-108, replace) */
+static void or_pexpand(or_pnode *nd, const float *pol81) {
+    int32_t leg[81];
+    int nl = or_legal_actions(&nd->s, leg);
+    float lp[81];
+    for (int i = 0; i < nl; ++i) lp[i] = pol81[leg[i]];
+    float sum = or_np_pairwise_sum_f32(lp, nl);
+    int p64 = 0;
+    if (sum > 0) {
+        for (int i = 0; i < nl; ++i) lp[i] = lp[i] / sum;
+    } else {
+        p64 = 1;
+    }
+    for (int i = 0; i < nd->nch; ++i) or_pnode_free(nd->ch[i]);
+    free(nd->ch);
+    nd->ch = (or_pnode **)malloc(sizeof(or_pnode *) * (size_t)(nl ? nl : 1));
+    nd->nch = nl;
+    for (int i = 0; i < nl; ++i) {
+        or_state ns;
+        or_next(&nd->s, leg[i], &ns);
+        or_pnode *c = or_pnode_new(&ns);
+        c->p = p64 ? 0.0f : lp[i];
+        c->p64 = p64;
+        c->nsib = nl;
+        nd->ch[i] = c;
+    }
+}
+
+/* backpropagate (:111-116); is_f32: the value is the network's np.float32 */
+static void or_pbackprop(or_pnode **path, int len, float value, int is_f32) {
+    for (int i = len - 1; i >= 0; --i) {
+        path[i]->w += value;
+        if (is_f32) path[i]->w_f32 = 1;
+        path[i]->n += 1;
+        value = -value;
+    }
+}
+
+/* next_child_node (:119-130) */
+static or_pnode *or_pnext_child(or_pnode *nd) {
+    int64_t t = 0;
+    for (int i = 0; i < nd->nch; ++i) t += nd->ch[i]->n;
+    const double sqt = sqrt((double)t);
+    double best = 0.0;
+    int bi = -1, best_nan = 0;
+    for (int i = 0; i < nd->nch; ++i) {
+        or_pnode *c = nd->ch[i];
+        double v;
+        if (c->p64) { /* np.float64 prior: the whole expression is float64 */
+            const double p = 1.0 / (double)c->nsib;
+            const double q = c->n ? (c->w_f32 ? (double)((-c->w) / (float)c->n) : (double)(-c->w) / (double)c->n) : 0.0;
+            v = q + ((1.0 * p) * sqt) / (double)(1 + c->n);
+        } else {        /* np.float32 prior: float32 ops, Python scalars cast to float32 */
+            const float q = c->n ? (c->w_f32 ? (-c->w) / (float)c->n : (float)((double)(-c->w) / (double)c->n)) : 0.0f;
+            const float u = ((1.0f * c->p) * (float)sqt) / (float)(1 + c->n);
+            v = (double)(q + u);
+        }
+        if (best_nan) continue;
+        if (v != v) { bi = i; best_nan = 1; continue; }
+        if (bi < 0 || v > best) { best = v; bi = i; }
+    }
+    return bi < 0 ? NULL : nd->ch[bi];
+}
+
+/* search_leaf (:88-101): terminal -> returns -(-1 if lose else 0), a Python int */
+static or_pnode *or_psearch_leaf(or_pnode *nd, or_pnode **path, int *len, float *value) {
+    for (;;) {
+        path[(*len)++] = nd;
+        if (or_is_done(&nd->s)) {
+            *value = or_is_lose(&nd->s) ? 1.0f : 0.0f;
+            return nd;
+        }
+        if (nd->nch <= 0) { *value = 0.0f; return nd; }
+        nd = or_pnext_child(nd);
+    }
+}
+
+/* pv_mcts_scores (:133-181) with PV_EVALUATE_COUNT / MCTS_BATCH_SIZE as parameters.
+ * Returns |root children|; scores_out = boltzman (Python floats) or one-hot. */
+int or_pv_mcts_scores_py(const or_state *root_s, double temperature, int evaluate_count, int batch_size,
+                         or_eval_fn eval, void *ctx, double *scores_out, int32_t *visits_out,
+                         or_search_stats *st_out) {
+    or_search_stats st;
+    memset(&st, 0, sizeof(st));
+    or_pnode *root = or_pnode_new(root_s);
+    st.nodes = 1;
+    int qcap = 64, qn = 0;
+    or_pnode **qleaf = (or_pnode **)malloc(sizeof(or_pnode *) * (size_t)qcap);
+    or_pnode ***qpath = (or_pnode ***)malloc(sizeof(or_pnode **) * (size_t)qcap);
+    int *qlen = (int *)malloc(sizeof(int) * (size_t)qcap);
+    or_pnode *path[OR_MAX_PATH];
+    for (int i = 0; i < evaluate_count; ++i) {
+        int len = 0;
+        float value;
+        or_pnode *leaf = or_psearch_leaf(root, path, &len, &value);
+        if (len - 1 > st.max_depth) st.max_depth = len - 1;
+        if (or_is_done(&leaf->s)) {
+            or_pbackprop(path, len, value, 0);
+            st.terminal++;
+            continue;
+        }
+        if (leaf->n == 0) {
+            if (qn == qcap) {
+                qcap *= 2;
+                qleaf = (or_pnode **)realloc(qleaf, sizeof(or_pnode *) * (size_t)qcap);
+                qpath = (or_pnode ***)realloc(qpath, sizeof(or_pnode **) * (size_t)qcap);
+                qlen = (int *)realloc(qlen, sizeof(int) * (size_t)qcap);
+            }
+            qleaf[qn] = leaf;
+            qpath[qn] = (or_pnode **)malloc(sizeof(or_pnode *) * (size_t)len);
+            memcpy(qpath[qn], path, sizeof(or_pnode *) * (size_t)len);
+            qlen[qn] = len;
+            qn++;
+        }
+        if (qn >= batch_size || i == evaluate_count - 1) {
+            if (qn > 0) {
+                st.flushes++;
+                float *pols = (float *)malloc(sizeof(float) * 81 * (size_t)qn);
+                float *vals = (float *)malloc(sizeof(float) * (size_t)qn);
+                for (int j = 0; j < qn; ++j) { /* one model call for the batch */
+                    float x[243];
+                    or_tensor_nchw(&qleaf[j]->s, x);
+                    eval(x, pols + 81 * j, vals + j, ctx);
+                    st.evals++;
+                }
+                for (int j = 0; j < qn; ++j) {
+                    or_pexpand(qleaf[j], pols + 81 * j);
+                    or_pbackprop(qpath[j], qlen[j], vals[j], 1);
+                    free(qpath[j]);
+                }
+                free(pols);
+                free(vals);
+                qn = 0;
+            }
+        }
+    }
+    int nout = root->nch > 0 ? root->nch : 0;
+    for (int i = 0; i < nout; ++i)
+        if (visits_out) visits_out[i] = root->ch[i]->n;
+    if (temperature == 0.0) { /* np.argmax, one-hot float64 */
+        int mi = 0;
+        for (int i = 1; i < nout; ++i)
+            if (root->ch[i]->n > root->ch[mi]->n) mi = i;
+        for (int i = 0; i < nout; ++i) scores_out[i] = 0.0;
+        if (nout) scores_out[mi] = 1.0;
+    } else {              /* boltzman: [x ** (1 / T)] then x / sum(xs), Python floats */
+        const double e = 1.0 / temperature;
+        double sum = 0.0;
+        for (int i = 0; i < nout; ++i) {
+            scores_out[i] = pow((double)root->ch[i]->n, e);
+        }
+        for (int i = 0; i < nout; ++i) sum += scores_out[i];
+        for (int i = 0; i < nout; ++i) scores_out[i] = scores_out[i] / sum;
+    }
+    for (int j = 0; j < qn; ++j) free(qpath[j]);
+    free(qleaf);
+    free(qpath);
+    free(qlen);
+    or_pnode_free(root);
+    if (st_out) *st_out = st;
+    return nout;
+}
+
+/* evaluate_network.py:33-51 play() for one game: players[0] moves when
+ * is_first_player(), each move pv_mcts_action (pv_mcts.py:184-188) drawing
+ * np.random.choice from RandomState(seed). Returns the first player's point
+ * (first_player_point, :26-30) * 2 (0, 1 or 2); actions_out gets the moves. */
+int or_evaluate_play(uint32_t seed, double temperature, int evaluate_count, int batch_size, or_eval_fn eval0,
+                     void *ctx0, or_eval_fn eval1, void *ctx1, int32_t *actions_out, int32_t *n_actions) {
+    or_mt mt;
+    or_mt_seed(&mt, seed);
+    or_state s;
+    or_state_initial(&s);
+    int na = 0;
+    while (!or_is_done(&s)) {
+        const int first = or_is_first_player(&s);
+        double sc[81];
+        int32_t leg[81];
+        int nl = or_legal_actions(&s, leg);
+        int n = or_pv_mcts_scores_py(&s, temperature, evaluate_count, batch_size, first ? eval0 : eval1,
+                                     first ? ctx0 : ctx1, sc, NULL, NULL);
+        if (n != nl) return -1;
+        int idx = or_np_choice(&mt, sc, n);
+        actions_out[na++] = leg[idx];
+        or_state ns;
+        or_next(&s, leg[idx], &ns);
+        s = ns;
+    }
+    *n_actions = na;
+    if (or_is_lose(&s)) return or_is_first_player(&s) ? 0 : 2;
+    return 1;
+}
+
+/* the hash evaluator with a salt (a second, different deterministic player) */
+void or_hash_eval_salted(const float *x, float *policy, float *value, uint64_t salt);
+void or_eval_hash_salted_cb(const float *x, float *policy, float *value, void *ctx) {
+    or_hash_eval_salted(x, policy, value, ctx ? *(const uint64_t *)ctx : 0ULL);
+}
+
+int or_pv_mcts_scores_py_hash(const or_state *root, double temperature, int evaluate_count, int batch_size,
+                              uint64_t salt, double *scores_out, int32_t *visits_out, or_search_stats *st) {
+    return or_pv_mcts_scores_py(root, temperature, evaluate_count, batch_size, or_eval_hash_salted_cb, &salt,
+                                scores_out, visits_out, st);
+}
+
+int or_evaluate_play_hash(uint32_t seed, double temperature, int evaluate_count, int batch_size, uint64_t salt0,
+                          uint64_t salt1, int32_t *actions_out, int32_t *n_actions) {
+    return or_evaluate_play(seed, temperature, evaluate_count, batch_size, or_eval_hash_salted_cb, &salt0,
+                            or_eval_hash_salted_cb, &salt1, actions_out, n_actions);
 }
 
 int or_state_size(void) { return (int)sizeof(or_state); }

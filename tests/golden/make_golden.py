@@ -11,9 +11,12 @@ Sources of truth used here:
     imported from /root/reference (self-play with numpy's global RNG seeded
     per game), driven by oracle.hashnp.HashModel;
   * the reference's dual_network.py (DualNetwork under torch.manual_seed(0),
-    CPU fp32) for the network I/O fixture.
+    CPU fp32) for the network I/O fixture;
+  * the reference's pv_mcts.py (Python PV-MCTS, its module constants set per
+    case) and evaluate_network.py play() with two salted hash players, numpy's
+    global RNG seeded per game (pvpy.npz, the arena path).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only pvpy]
 """
 import json
 import os
@@ -187,8 +190,87 @@ def gen_network(n_states=24):
     return {"x": x.numpy(), "policy": p.numpy(), "value": v.numpy(), "param_sums": fp, "param_names": names}
 
 
+PY_CONFIGS = [(50, 8), (50, 1), (30, 3), (10, 2), (1, 1), (7, 100), (64, 64)]
+ARENA_SALTS = (0, 0x5EED5EED12345678)
+
+
+def gen_pvpy(positions, n_games=8, base_seed=4321):
+    """pv_mcts.py (Python semantics) scores + evaluate_network.play games."""
+    sys.path[:0] = [ref.REF_DIR, REF]
+    import uttt_cpp  # reference build
+    import pv_mcts  # reference Python MCTS
+    import evaluate_network  # reference arena
+    from oracle.hashnp import make_hash_model
+    model = make_hash_model(0)
+    out = {"pos_" + k: [] for k in ("pieces", "enemy", "main_p", "main_e", "active")}
+    for st in positions:
+        p, e, m, me, a = pack(st)
+        for k, v in (("pieces", p), ("enemy", e), ("main_p", m), ("main_e", me), ("active", a)):
+            out["pos_" + k].append(v)
+    res = {"scores": [], "n": [], "pos": [], "sims": [], "batch": [], "temp": []}
+    saved = (pv_mcts.PV_EVALUATE_COUNT, pv_mcts.MCTS_BATCH_SIZE)
+    try:
+        for pi, st in enumerate(positions):
+            state = uttt_cpp.State(st[0].tolist(), st[1].tolist(), st[2].tolist(), st[3].tolist(), int(st[4]))
+            for (S, B) in PY_CONFIGS:
+                pv_mcts.PV_EVALUATE_COUNT, pv_mcts.MCTS_BATCH_SIZE = S, B
+                for tau in TEMPERATURES:
+                    row = np.zeros(81, np.float64)
+                    try:
+                        sc = np.asarray(pv_mcts.pv_mcts_scores(model, state, tau), np.float64)
+                        row[:sc.size] = sc
+                    except ZeroDivisionError:  # boltzman over all-zero visits (S <= B: only the
+                        sc = None              # root was ever reached); recorded as n = -1
+                    if sc is None:
+                        res["scores"].append(row)
+                        for k, v in (("n", -1), ("pos", pi), ("sims", S), ("batch", B), ("temp", tau)):
+                            res[k].append(v)
+                        continue
+                    for k, v in (("scores", row), ("n", sc.size), ("pos", pi), ("sims", S), ("batch", B),
+                                 ("temp", tau)):
+                        res[k].append(v)
+    finally:
+        pv_mcts.PV_EVALUATE_COUNT, pv_mcts.MCTS_BATCH_SIZE = saved
+    out = {k: np.asarray(v) for k, v in out.items()}
+    out.update({k: np.asarray(v) for k, v in res.items()})
+    # arena: game g = evaluate_network.play after np.random.seed(base_seed + g); even games
+    # start with player 0 (salt ARENA_SALTS[0]), odd games with player 1 (evaluate_network.py:78-82)
+    players = [pv_mcts.pv_mcts_action(make_hash_model(s), 1.0) for s in ARENA_SALTS]
+    A, L, PT, SD = [], [], [], []
+    real_choice = np.random.choice
+
+    def recording_choice(*args, **kw):
+        r = real_choice(*args, **kw)
+        A.append(int(r))
+        return r
+
+    np.random.choice = recording_choice
+    try:
+        for g in range(n_games):
+            np.random.seed(base_seed + g)
+            n0 = len(A)
+            acts = players if g % 2 == 0 else list(reversed(players))
+            PT.append(float(evaluate_network.play(acts)))
+            L.append(len(A) - n0)
+            SD.append(base_seed + g)
+    finally:
+        np.random.choice = real_choice
+    out.update({"arena_actions": np.asarray(A, np.int8), "arena_lengths": np.asarray(L, np.int32),
+                "arena_points": np.asarray(PT, np.float64), "arena_seeds": np.asarray(SD, np.int64),
+                "arena_salts": np.asarray(ARENA_SALTS, np.uint64)})
+    return out
+
+
 def main():
     assert ref.available(), "build oracle/_ref first: make -C oracle"
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "pvpy":
+        rules = dict(np.load(os.path.join(HERE, "rules.npz")))
+        positions = sample_positions(rules) + [initial(), win_in_one()]
+        pv = gen_pvpy(positions)
+        np.savez_compressed(os.path.join(HERE, "pvpy.npz"), **pv)
+        print("pvpy:", len(pv["n"]), "searches;", len(pv["arena_lengths"]), "arena games,",
+              int(pv["arena_lengths"].sum()), "moves; points", pv["arena_points"].tolist())
+        return
     rules, strings, q7 = gen_rules()
     np.savez_compressed(os.path.join(HERE, "rules.npz"), **rules)
     with open(os.path.join(HERE, "to_string.json"), "w") as f:
@@ -205,6 +287,9 @@ def main():
     nn = gen_network()
     np.savez_compressed(os.path.join(HERE, "network.npz"), **nn)
     print("network:", nn["x"].shape[0], "states")
+    pv = gen_pvpy(positions)
+    np.savez_compressed(os.path.join(HERE, "pvpy.npz"), **pv)
+    print("pvpy:", len(pv["n"]), "searches;", len(pv["arena_lengths"]), "arena games")
 
 
 if __name__ == "__main__":

@@ -136,3 +136,42 @@ def test_oracle_vs_compiled_reference_live(oracle_lib):
                 checked += 1
             s = s.next(rng.choice(legal))
     assert checked > 50
+
+
+# ---------------------------------------------------------------- arena path --
+def _pos_state(core, d, i):
+    return core.OrState.from_arrays(d["pos_pieces"][i].reshape(9, 9), d["pos_enemy"][i].reshape(9, 9),
+                                    d["pos_main_p"][i], d["pos_main_e"][i], int(d["pos_active"][i]))
+
+
+def test_oracle_python_mcts_matches_reference_pv_mcts(oracle_lib):
+    """or_pv_mcts_scores_py == the reference's pv_mcts.pv_mcts_scores (Python semantics,
+    SURVEY App. B) on 42 positions x 7 (S, B) x 3 temperatures, float64 bits; where the
+    reference raises ZeroDivisionError (S <= B) the oracle reports no root child visit."""
+    core = oracle_lib
+    d = golden("pvpy.npz")
+    for r in range(len(d["n"])):
+        st = _pos_state(core, d, int(d["pos"][r]))
+        sc, vis, _ = core.pv_mcts_scores_py_hash(st, float(d["temp"][r]), int(d["sims"][r]), int(d["batch"][r]))
+        n = int(d["n"][r])
+        if n < 0:
+            assert sc is None, r
+            continue
+        assert sc is not None and sc.size == n, r
+        assert np.array_equal(sc.view(np.uint64), d["scores"][r, :n].view(np.uint64)), r
+
+
+def test_oracle_arena_games_match_reference(oracle_lib):
+    """evaluate_network.play with two salted hash players, np.random.seed(seed) per game:
+    same moves and same first-player points as the reference."""
+    core = oracle_lib
+    d = golden("pvpy.npz")
+    s0, s1 = (int(x) for x in d["arena_salts"])
+    off = 0
+    for g in range(len(d["arena_lengths"])):
+        first, second = (s0, s1) if g % 2 == 0 else (s1, s0)
+        point, acts = core.evaluate_play_hash(int(d["arena_seeds"][g]), first, second)
+        n = int(d["arena_lengths"][g])
+        assert np.array_equal(acts, d["arena_actions"][off:off + n].astype(np.int32)), g
+        assert point == d["arena_points"][g], g
+        off += n
