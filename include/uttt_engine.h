@@ -103,11 +103,24 @@ int uttt_engine_own_stream(uttt_engine_t *eng, void **stream);
 /* Device bytes held by the engine. */
 int64_t uttt_engine_device_bytes(const uttt_engine_t *eng);
 
+/* Search semantics for uttt_search_begin_mode:
+ *  UTTT_SEMANTICS_CPP  cpp/uttt_mcts.cpp (pv_mcts_cpp / self_play_cpp): root
+ *                      pre-expanded uniform, expand appends k blocks, f32 PUCT;
+ *  UTTT_SEMANTICS_PY   pv_mcts.py (evaluate_network / evaluate_best_player):
+ *                      root evaluated by the first flush, expand replaces,
+ *                      PUCT as NumPy 2 evaluates the Python expression
+ *                      (float32 with sqrt in double; float64 where the
+ *                      all-zero-prior fallback made the priors float64). */
+#define UTTT_SEMANTICS_CPP 0
+#define UTTT_SEMANTICS_PY 1
 /* Start a search of n_trees independent trees (pv_mcts_scores,
  * uttt_mcts.cpp:92-103: root expanded with uniform priors 1/|legal|).
  * roots: host array of n_trees states. */
 int uttt_search_begin(uttt_engine_t *eng, const uttt_state_t *roots, int32_t n_trees, int32_t evaluate_count,
                       int32_t batch_size);
+/* The same with explicit semantics (replaces pv_mcts.py:133-181 when PY). */
+int uttt_search_begin_mode(uttt_engine_t *eng, const uttt_state_t *roots, int32_t n_trees, int32_t evaluate_count,
+                           int32_t batch_size, int32_t semantics);
 
 /* One round of descents (uttt_mcts.cpp:109-127). Writes the pending leaves'
  * network inputs, NCHW (n,3,9,9) f32, to device memory nn_input (room for

@@ -403,3 +403,68 @@ def test_winograd_conv_matches_torch_fp32(gpu):
                 want = torch.relu(ref + (res.double() if res is not None else 0)).float()
                 err = (y - want).abs().max().item()
                 assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, f3, res is None, err)
+
+
+# ---------------------------------------------------------------- arena path --
+def test_py_semantics_search_matches_reference_pv_mcts(gpu):
+    """UTTT_SEMANTICS_PY on the engine == the reference's pv_mcts.pv_mcts_scores
+    (tests/golden/pvpy.npz): 42 positions x 7 (S, B) x 3 temperatures, all searched
+    together per configuration, float64 score bits; ZeroDivisionError where the
+    reference raises it (S <= B)."""
+    from uttt_amd.arena import PvMcts, scores_from_visits
+    import uttt_cpp
+    d = golden("pvpy.npz")
+    npos = len(d["pos_active"])
+    states = [uttt_cpp.State(d["pos_pieces"][i].reshape(9, 9).tolist(), d["pos_enemy"][i].reshape(9, 9).tolist(),
+                             d["pos_main_p"][i].tolist(), d["pos_main_e"][i].tolist(), int(d["pos_active"][i]))
+              for i in range(npos)]
+    pm = PvMcts(npos, 64)
+    ev = gpu.HashEvaluator(pm.engine)
+    cfgs = sorted(set(zip(d["sims"].tolist(), d["batch"].tolist())))
+    for S, B in cfgs:
+        visits = pm.visits(states, ev, S, B)
+        for r in np.nonzero((d["sims"] == S) & (d["batch"] == B))[0]:
+            v = visits[int(d["pos"][r])]
+            n = int(d["n"][r])
+            if n < 0:
+                with pytest.raises(ZeroDivisionError):
+                    scores_from_visits(v, float(d["temp"][r]))
+                continue
+            sc = np.asarray(scores_from_visits(v, float(d["temp"][r])), np.float64)
+            assert sc.size == n, (S, B, r)
+            assert np.array_equal(sc.view(np.uint64), d["scores"][r, :n].view(np.uint64)), (S, B, r)
+
+
+def test_py_semantics_random_positions_match_oracle(gpu, oracle_lib):
+    """Fresh random positions at several (S, B), engine vs the pinned oracle restatement."""
+    from uttt_amd.arena import PvMcts
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 200, seed=29)
+    pm = PvMcts(len(roots), 200)
+    ev = gpu.HashEvaluator(pm.engine)
+    for S, B in [(50, 8), (200, 4), (33, 5), (50, 1)]:
+        visits = pm.visits(roots, ev, S, B)
+        for i in range(0, len(ostates), 3):
+            _, vi, _ = core.pv_mcts_scores_py_hash(ostates[i], 1.0, S, B)
+            assert np.array_equal(visits[i], vi), (S, B, i)
+
+
+def test_arena_matches_reference_games(gpu):
+    """uttt_amd.arena.evaluate_network with the two salted hash players of the fixture:
+    every game's moves and first-player point equal the reference's evaluate_network
+    play() after np.random.seed(seed + g); model0's average point follows."""
+    from oracle.hashnp import make_hash_model
+    from uttt_amd import arena
+    d = golden("pvpy.npz")
+    s0, s1 = (int(x) for x in d["arena_salts"])
+    ng = len(d["arena_lengths"])
+    avg, points, actions = arena.evaluate_network(make_hash_model(s0), make_hash_model(s1), ng, 1.0,
+                                                  int(d["arena_seeds"][0]))
+    off = 0
+    for g in range(ng):
+        n = int(d["arena_lengths"][g])
+        assert actions[g] == d["arena_actions"][off:off + n].astype(int).tolist(), g
+        assert points[g] == d["arena_points"][g], g
+        off += n
+    want = sum(p if g % 2 == 0 else 1 - p for g, p in enumerate(d["arena_points"].tolist())) / ng
+    assert avg == want

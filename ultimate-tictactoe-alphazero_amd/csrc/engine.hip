@@ -106,13 +106,17 @@ struct Trees {
     int32_t n_trees;
     int32_t sims;
     int32_t batch;
+    int32_t py;  // 1: pv_mcts.py semantics (arena), 0: cpp/uttt_mcts.cpp (self-play)
 };
 
 // link.y packing
 __host__ __device__ __forceinline__ uint32_t pack_meta(uint32_t k, uint32_t L, uint32_t action) {
     return (k & 0xFFFFu) | ((L & 0xFFu) << 16) | ((action & 0xFFu) << 24);
 }
-__host__ __device__ __forceinline__ int meta_k(uint32_t y) { return (int)(y & 0xFFFFu); }
+__host__ __device__ __forceinline__ int meta_k(uint32_t y) { return (int)(y & 0x3FFFu); }
+// py semantics only (pv_mcts.py, NumPy 2 scalar promotion):
+constexpr uint32_t kMetaP64 = 0x4000u;   // this node's children carry float64 uniform priors
+constexpr uint32_t kMetaWF32 = 0x8000u;  // this node's w has become np.float32 (a network value)
 __host__ __device__ __forceinline__ int meta_L(uint32_t y) { return (int)((y >> 16) & 0xFFu); }
 __host__ __device__ __forceinline__ int meta_action(uint32_t y) { return (int)(y >> 24); }
 
@@ -126,6 +130,18 @@ __device__ __forceinline__ uint64_t lanes_below() {
 
 // Wave-wide arg-max: larger value wins, equal values -> smaller index
 // (the reference's strict '>' scan in child order, uttt_mcts.cpp:69-78).
+__device__ __forceinline__ void wave_argmax_d(double &v, int &i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double ov = __shfl_xor(v, off);
+        const int oi = __shfl_xor(i, off);
+        if (ov > v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
 __device__ __forceinline__ void wave_argmax(float &v, int &i) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -273,8 +289,39 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
 // :38-43); back up v k times along path[0..depth] (:47-54, leaf first, sign
 // flipping upward). Lane d holds path[d] in path_lo and path[64+d] in path_hi.
 // Returns false without writing when the node pool would overflow.
+// py (pv_mcts.py:46-56, :104-116): priors normalised by np.sum (float32 pairwise),
+// all-zero -> float64 uniform (kMetaP64); ONE child block (expand replaces, and
+// the k copies of a flush expand the same children); every node on the path
+// gets a network value, so its w becomes float32 (kMetaWF32).
+__device__ float np_sum_f32_legal(float p0, float p1, uint64_t b0, uint64_t b1, int L) {
+    // numpy pairwise_sum for float32, n <= 128: 8 strided accumulators, then the tail
+    auto nth = [&](int idx) -> float {  // idx-th legal prior in action order (wave-uniform)
+        const int c0 = __popcll(b0);
+        uint64_t bits = idx < c0 ? b0 : b1;
+        int r = idx < c0 ? idx : idx - c0;
+        for (; r > 0; --r) bits &= bits - 1ull;
+        const int l = __builtin_ctzll(bits);
+        return idx < c0 ? readlane_f(p0, l) : readlane_f(p1, l);
+    };
+    if (L < 8) {
+        float res = 0.0f;
+        for (int i = 0; i < L; ++i) res += nth(i);
+        return res;
+    }
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = nth(j);
+    const int main_end = L - L % 8;
+    for (int i = 8; i < main_end; i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += nth(i + j);
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int i = main_end; i < L; ++i) res += nth(i);
+    return res;
+}
+
 __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi, int k,
-                              const uttt_state_t &s, const float *pol, float v, int &node_count) {
+                              const uttt_state_t &s, const float *pol, float v, int &node_count, bool py = false) {
     const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
@@ -283,18 +330,24 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
     const int L = __popcll(b0) + __popcll(b1);
     const int nb = node_count;
-    if ((int64_t)nb + (int64_t)k * L > pool.cap || L == 0) return false;
+    const int blocks = py ? 1 : k;
+    if ((int64_t)nb + (int64_t)blocks * L > pool.cap || L == 0) return false;
     const int i0 = __popcll(b0 & lanes_below());
     const int i1 = __popcll(b0) + __popcll(b1 & lanes_below());
     const float p0 = l0 ? pol[lane] : 0.0f;
     const float p1 = l1 ? pol[64 + lane] : 0.0f;
     float sum = 0.0f;
-    for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
-    for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+    if (py) {
+        sum = np_sum_f32_legal(p0, p1, b0, b1, L);
+    } else {
+        for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
+        for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+    }
     const float un = 1.0f / (float)L;
+    const bool p64 = py && !(sum > 0);  // np.ones(float) / L: float64 priors
     const float q0 = sum > 0 ? p0 / sum : un;
     const float q1 = sum > 0 ? p1 / sum : un;
-    for (int j = 0; j < k; ++j) {
+    for (int j = 0; j < blocks; ++j) {
         const size_t blk = base + nb + (size_t)j * L;
         if (l0) {
             pool.n[blk + i0] = 0;
@@ -315,6 +368,7 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
         for (int j = 0; j < k; ++j) w += x;
         pool.w[base + path_lo] = w;
         pool.n[base + path_lo] += k;
+        if (py && lane < depth) pool.link[base + path_lo].y |= kMetaWF32;
     }
     if (lane + 64 <= depth) {
         float w = pool.w[base + path_hi];
@@ -322,13 +376,15 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
         for (int j = 0; j < k; ++j) w += x;
         pool.w[base + path_hi] = w;
         pool.n[base + path_hi] += k;
+        if (py && lane + 64 < depth) pool.link[base + path_hi].y |= kMetaWF32;
     }
     if (lane == 0) {
         const uint2 old = pool.link[base + node];
-        pool.link[base + node] =
-            make_uint2((uint32_t)nb, pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y)));
+        uint32_t meta = pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y));
+        if (py) meta |= kMetaWF32 | (p64 ? kMetaP64 : 0u);
+        pool.link[base + node] = make_uint2((uint32_t)nb, meta);
     }
-    node_count = nb + k * L;
+    node_count = nb + blocks * L;
     return true;
 }
 
@@ -344,6 +400,23 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
     const size_t base = (size_t)t * pool.cap;
     uint32_t m[3];
     legal_mask(s, m);
+    if (tr.py) {  // pv_mcts.py:134: the root is a plain unexpanded node (evaluated by the first flush)
+        const bool any = __ballot(bit_of(m, lane) != 0u) != 0ull || __ballot(lane < 17 && bit_of(m, 64 + lane) != 0u);
+        if (lane == 0) {
+            pool.n[base] = 0;
+            pool.w[base] = 0.0f;
+            pool.p[base] = 0.0f;
+            pool.link[base] = make_uint2(0u, pack_meta(0, 0, 0xFFu));
+            tr.root[t] = s;
+            TreeCtl c;
+            c.sims_done = 0;
+            c.node_count = 1;
+            c.status = (on && any) ? kLive : 0;
+            c.pad = 0;
+            tr.ctl[t] = c;
+        }
+        return;
+    }
     const bool l0 = on && bit_of(m, lane);
     const bool l1 = on && lane < 17 && bit_of(m, 64 + lane);
     const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
@@ -408,28 +481,59 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
             uint2 lk = LK[0];
             bool fail = false;
             for (;;) {
-                const int cnt = meta_k(lk.y) * meta_L(lk.y);
+                const int cnt = tr.py ? meta_L(lk.y) : meta_k(lk.y) * meta_L(lk.y);
                 if (cnt == 0) break;
                 const int first = (int)lk.x;
-                const int kself = node == 0 ? 0 : meta_k(lk.y);
+                const int kself = (node == 0 && !tr.py) ? 0 : meta_k(lk.y);
                 const int total = N[node] - kself;  // == sum of children's visits
-                const float sq = sqrtf((float)total);
-                float best = -1e9f;
                 int bi = kNone;
-                for (int c = lane; c < cnt; c += kWave) {
-                    const int cn = N[first + c];
-                    const float cw = W[first + c];
-                    const float cp = P[first + c];
-                    // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off)
-                    const float q = (cn > 0) ? (-cw / (float)cn) : 0.0f;
-                    const float u = cp * sq / (float)(1 + cn);
-                    const float v = q + u;
-                    if (v > best) {
-                        best = v;
-                        bi = c;
+                if (!tr.py) {
+                    const float sq = sqrtf((float)total);
+                    float best = -1e9f;
+                    for (int c = lane; c < cnt; c += kWave) {
+                        const int cn = N[first + c];
+                        const float cw = W[first + c];
+                        const float cp = P[first + c];
+                        // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off)
+                        const float q = (cn > 0) ? (-cw / (float)cn) : 0.0f;
+                        const float u = cp * sq / (float)(1 + cn);
+                        const float v = q + u;
+                        if (v > best) {
+                            best = v;
+                            bi = c;
+                        }
                     }
+                    wave_argmax(best, bi);
+                } else {
+                    // pv_mcts.py:120-130 under NumPy 2 promotion: float32 ops with sqrt(t)
+                    // in double, or float64 throughout when the priors are float64;
+                    // np.argmax: first maximum, a NaN counts as the maximum.
+                    const bool p64 = (lk.y & kMetaP64) != 0u;
+                    const double sqt = sqrt((double)total);
+                    const float sq = (float)sqt;
+                    const double pu = 1.0 / (double)meta_L(lk.y);
+                    double best = -HUGE_VAL;
+                    for (int c = lane; c < cnt; c += kWave) {
+                        const int cn = N[first + c];
+                        const float cw = W[first + c];
+                        const bool wf = (LK[first + c].y & kMetaWF32) != 0u;
+                        double v;
+                        if (p64) {
+                            const double q = cn > 0 ? (wf ? (double)((-cw) / (float)cn) : (double)(-cw) / (double)cn) : 0.0;
+                            v = q + ((1.0 * pu) * sqt) / (double)(1 + cn);
+                        } else {
+                            const float q = cn > 0 ? (wf ? (-cw) / (float)cn : (float)((double)(-cw) / (double)cn)) : 0.0f;
+                            const float u = ((1.0f * P[first + c]) * sq) / (float)(1 + cn);
+                            v = (double)(q + u);
+                        }
+                        if (v != v) v = HUGE_VAL;
+                        if (bi == kNone || v > best) {
+                            best = v;
+                            bi = c;
+                        }
+                    }
+                    wave_argmax_d(best, bi);
                 }
-                wave_argmax(best, bi);
                 bi = __builtin_amdgcn_readfirstlane(bi);
                 bytes += 12ull * (unsigned long long)cnt + 8ull;
                 if (bi == kNone) {  // every child NaN: the reference would dereference null
@@ -478,7 +582,8 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
             const int k = min(tr.batch, tr.sims - sims_done);
             float *cv = s_hit[threadIdx.x >> 6];
             if (cache_lookup(cache, s, cv)) {  // the flush's evaluation is already known: apply it now
-                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count)) {
+                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count,
+                                   tr.py != 0)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
                 }
@@ -585,7 +690,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
     if (!per_copy) {
         const float *pol = policy + (int64_t)slot * pld;
         const float v = value[(int64_t)slot * vld];
-        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, pol, v, ctl.node_count)) {
+        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, pol, v, ctl.node_count, tr.py != 0)) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
@@ -1303,10 +1408,19 @@ static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, in
 }
 
 int uttt_search_begin(uttt_engine_t *e, const uttt_state_t *roots, int32_t n_trees, int32_t sims, int32_t batch) {
-    if (!e || !roots) return UTTT_ERR_ARG;
+    return uttt_search_begin_mode(e, roots, n_trees, sims, batch, UTTT_SEMANTICS_CPP);
+}
+
+int uttt_search_begin_mode(uttt_engine_t *e, const uttt_state_t *roots, int32_t n_trees, int32_t sims, int32_t batch,
+                           int32_t semantics) {
+    if (!e || !roots || (semantics != UTTT_SEMANTICS_CPP && semantics != UTTT_SEMANTICS_PY)) {
+        set_error("uttt_search_begin_mode: bad arguments (semantics 0 = cpp, 1 = py)");
+        return UTTT_ERR_ARG;
+    }
     HIP_TRY(hipSetDevice(e->device));
     int rc = search_begin_common(e, n_trees, sims, batch);
     if (rc) return rc;
+    e->tr.py = semantics == UTTT_SEMANTICS_PY ? 1 : 0;
     e->selfplay = false;
     HIP_TRY(hipMemcpyAsync(e->tr.leaf, roots, sizeof(uttt_state_t) * n_trees, hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_begin, dim3(grid_waves(n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
@@ -1381,6 +1495,10 @@ int uttt_search_apply(uttt_engine_t *e, const float *policy, int64_t pld, const 
     if (e->phase != 2) {
         set_error("uttt_search_apply: no pending leaves (call uttt_search_select)");
         return UTTT_ERR_ORDER;
+    }
+    if (per_copy && e->tr.py) {
+        set_error("uttt_search_apply: per_copy is the cpp call pattern; py semantics take one result per leaf");
+        return UTTT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(e->device));
     const int n = e->n_pending;
@@ -1498,6 +1616,7 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipSetDevice(e->device));
     const int slots = e->max_trees;
     int rc = search_begin_common(e, slots, sims, batch);
+    e->tr.py = 0;  // self-play is the cpp/uttt_mcts.cpp path
     if (rc) return rc;
     e->phase = 0;  // move_begin first
     SelfPlay &sp = e->sp;

@@ -63,6 +63,7 @@ SIGNATURES = {
     "uttt_engine_set_stream": (ctypes.c_int, [_P, _P]),
     "uttt_engine_device_bytes": (ctypes.c_int64, [_P]),
     "uttt_search_begin": (ctypes.c_int, [_P, _SP, _I32, _I32, _I32]),
+    "uttt_search_begin_mode": (ctypes.c_int, [_P, _SP, _I32, _I32, _I32, _I32]),
     "uttt_search_select": (ctypes.c_int, [_P, _P, _I32P]),
     "uttt_search_pending": (ctypes.c_int, [_P, _SP, _I32P]),
     "uttt_search_apply": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I32, _I32]),

@@ -80,10 +80,13 @@ class Engine:
         return int(self.lib.uttt_engine_device_bytes(self.h))
 
     # ---------------------------------------------------------------- search --
-    def search_begin(self, roots, evaluate_count=50, batch_size=8):
+    SEMANTICS = {"cpp": 0, "py": 1}
+
+    def search_begin(self, roots, evaluate_count=50, batch_size=8, semantics="cpp"):
+        """semantics "cpp": cpp/uttt_mcts.cpp (pv_mcts_cpp, self-play); "py": pv_mcts.py (arena)."""
         roots = as_states(roots)
-        check(self.lib.uttt_search_begin(self.h, roots.ctypes.data_as(ctypes.POINTER(UtttState)), len(roots),
-                                         int(evaluate_count), int(batch_size)))
+        check(self.lib.uttt_search_begin_mode(self.h, roots.ctypes.data_as(ctypes.POINTER(UtttState)), len(roots),
+                                              int(evaluate_count), int(batch_size), self.SEMANTICS[semantics]))
         self.n_trees = len(roots)
 
     def select(self, nn_input=None):

@@ -64,10 +64,10 @@ class BatchedSearch:
         self.x = torch.zeros((max_trees, 3, 9, 9), dtype=torch.float32, device=dev)
         self.rounds = 0
 
-    def run(self, roots, evaluator, evaluate_count=50, batch_size=8):
+    def run(self, roots, evaluator, evaluate_count=50, batch_size=8, semantics="cpp"):
         e = self.engine
         e.use_stream()
-        e.search_begin(roots, evaluate_count, batch_size)
+        e.search_begin(roots, evaluate_count, batch_size, semantics)
         self.rounds = 0
         x = self.x if getattr(evaluator, "needs_input", True) else None
         while True:
