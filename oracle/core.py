@@ -140,6 +140,9 @@ def lib():
                                                 F64P, I32P, ctypes.POINTER(SearchStats)]
         L.or_evaluate_play_hash.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_uint64, ctypes.c_uint64, I32P, I32P]
+        L.or_self_play_game_py_hash.argtypes = [ctypes.c_uint32, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_uint64, F32P, F64P, ctypes.POINTER(ctypes.c_int8),
+                                                ctypes.c_int]
         L.or_np_pairwise_sum_f32.argtypes = [F32P, ctypes.c_int64]
         L.or_np_pairwise_sum_f32.restype = ctypes.c_float
         L.or_mt_seed.argtypes = [ctypes.POINTER(MT), ctypes.c_uint32]
@@ -223,6 +226,20 @@ def evaluate_play_hash(seed, salt_first, salt_second, temperature=1.0, evaluate_
     if r < 0:
         raise RuntimeError("or_evaluate_play_hash: scores / legal length mismatch")
     return r / 2.0, acts[:na.value].copy()
+
+
+def self_play_game_py_hash(seed, temperature=1.0, evaluate_count=50, batch_size=8, salt=0, max_plies=81):
+    """self_play.py play() after np.random.seed(seed), hash evaluator -> dict of per-ply arrays."""
+    t = np.zeros((max_plies, 243), np.float32)
+    p = np.zeros((max_plies, 81), np.float64)
+    v = np.zeros(max_plies, np.int8)
+    n = lib().or_self_play_game_py_hash(ctypes.c_uint32(seed), float(temperature), int(evaluate_count),
+                                        int(batch_size), ctypes.c_uint64(salt), t.ctypes.data_as(F32P),
+                                        p.ctypes.data_as(F64P), v.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)),
+                                        max_plies)
+    if n < 0:
+        raise RuntimeError("or_self_play_game_py_hash failed")
+    return {"tensors": t[:n], "policies": p[:n], "values": v[:n]}
 
 
 def np_pairwise_sum_f32(a):

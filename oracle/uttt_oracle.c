@@ -819,5 +819,46 @@ int or_evaluate_play_hash(uint32_t seed, double temperature, int evaluate_count,
                             or_eval_hash_salted_cb, &salt1, actions_out, n_actions);
 }
 
+/* self_play.py:66-99 play(model) for one game, RandomState(seed): per ply the HWC
+ * input, policies (float64, 0 for illegal actions) and value (first_player_value
+ * at ply 0, then alternating, :20-25 / :94-97). Returns plies. */
+int or_self_play_game_py(uint32_t seed, double temperature, int evaluate_count, int batch_size, or_eval_fn eval,
+                         void *ctx, float *tensors_hwc, double *policies, int8_t *values, int max_plies) {
+    or_mt mt;
+    or_mt_seed(&mt, seed);
+    or_state s;
+    or_state_initial(&s);
+    int np_ = 0;
+    while (!or_is_done(&s)) {
+        if (np_ >= max_plies) return -1;
+        double sc[81];
+        int32_t leg[81];
+        int nl = or_legal_actions(&s, leg);
+        int n = or_pv_mcts_scores_py(&s, temperature, evaluate_count, batch_size, eval, ctx, sc, NULL, NULL);
+        if (n != nl) return -2;
+        double *pol = policies + 81 * (size_t)np_;
+        for (int a = 0; a < 81; ++a) pol[a] = 0.0;
+        for (int i = 0; i < nl; ++i) pol[leg[i]] = sc[i];
+        or_tensor_hwc(&s, tensors_hwc + 243 * (size_t)np_);
+        int idx = or_np_choice(&mt, sc, n);
+        or_state ns;
+        or_next(&s, leg[idx], &ns);
+        s = ns;
+        ++np_;
+    }
+    int v = or_is_lose(&s) ? (or_is_first_player(&s) ? -1 : 1) : 0;
+    for (int i = 0; i < np_; ++i) {
+        values[i] = (int8_t)v;
+        v = -v;
+    }
+    return np_;
+}
+
+int or_self_play_game_py_hash(uint32_t seed, double temperature, int evaluate_count, int batch_size, uint64_t salt,
+                              float *tensors_hwc, double *policies, int8_t *values, int max_plies) {
+    return or_self_play_game_py(seed, temperature, evaluate_count, batch_size, or_eval_hash_salted_cb, &salt,
+                                tensors_hwc, policies, values, max_plies);
+}
+
 int or_state_size(void) { return (int)sizeof(or_state); }
 int or_search_stats_size(void) { return (int)sizeof(or_search_stats); }

@@ -258,6 +258,23 @@ def gen_pvpy(positions, n_games=8, base_seed=4321):
     out.update({"arena_actions": np.asarray(A, np.int8), "arena_lengths": np.asarray(L, np.int32),
                 "arena_points": np.asarray(PT, np.float64), "arena_seeds": np.asarray(SD, np.int64),
                 "arena_salts": np.asarray(ARENA_SALTS, np.uint64)})
+    # self_play.py (the Python self-play, BASELINE configs[0]): play(model) after np.random.seed(seed + g)
+    import self_play  # reference module
+    T, P, V, SL, SS, DT = [], [], [], [], [], set()
+    for g in range(6):
+        np.random.seed(base_seed + 100 + g)
+        h = self_play.play(model)
+        for rec in h:
+            x = np.asarray(rec[0])
+            DT.add(str(x.dtype))
+            T.append(x.reshape(243).astype(np.uint8))
+            P.append(np.asarray(rec[1], np.float64))
+            V.append(int(rec[2]))
+        SL.append(len(h))
+        SS.append(base_seed + 100 + g)
+    assert DT == {"float64"}, DT
+    out.update({"sp_tensors": np.asarray(T), "sp_policies": np.asarray(P), "sp_values": np.asarray(V, np.int8),
+                "sp_lengths": np.asarray(SL, np.int32), "sp_seeds": np.asarray(SS, np.int64)})
     return out
 
 
@@ -269,7 +286,8 @@ def main():
         pv = gen_pvpy(positions)
         np.savez_compressed(os.path.join(HERE, "pvpy.npz"), **pv)
         print("pvpy:", len(pv["n"]), "searches;", len(pv["arena_lengths"]), "arena games,",
-              int(pv["arena_lengths"].sum()), "moves; points", pv["arena_points"].tolist())
+              int(pv["arena_lengths"].sum()), "moves; points", pv["arena_points"].tolist(), "; self_play.py:",
+              len(pv["sp_lengths"]), "games,", int(pv["sp_lengths"].sum()), "plies")
         return
     rules, strings, q7 = gen_rules()
     np.savez_compressed(os.path.join(HERE, "rules.npz"), **rules)

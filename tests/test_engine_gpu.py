@@ -468,3 +468,33 @@ def test_arena_matches_reference_games(gpu):
         off += n
     want = sum(p if g % 2 == 0 else 1 - p for g, p in enumerate(d["arena_points"].tolist())) / ng
     assert avg == want
+
+
+def test_python_self_play_matches_reference(gpu):
+    """arena.self_play_py (self_play.py, BASELINE configs[0], all games concurrent) ==
+    the reference's self_play.play after np.random.seed(seed + g): inputs, float64
+    policy bits, values; and the drop-in self_play.play on the global RNG for one game."""
+    from oracle.hashnp import make_hash_model
+    from uttt_amd import arena
+    d = golden("pvpy.npz")
+    ng = len(d["sp_lengths"])
+    games = arena.self_play_py(make_hash_model(0), ng, int(d["sp_seeds"][0]))
+    off = 0
+    for g in range(ng):
+        n = int(d["sp_lengths"][g])
+        sl = slice(off, off + n)
+        h = games[g]
+        assert len(h) == n, g
+        assert all(r[0].dtype == np.float64 for r in h)
+        assert np.array_equal(np.asarray([r[0].reshape(243) for r in h]).astype(np.uint8), d["sp_tensors"][sl]), g
+        assert np.array_equal(np.asarray([r[1] for r in h], np.float64).view(np.uint64),
+                              d["sp_policies"][sl].view(np.uint64)), g
+        assert [r[2] for r in h] == d["sp_values"][sl].astype(int).tolist(), g
+        off += n
+    import self_play
+    np.random.seed(int(d["sp_seeds"][1]))
+    h = self_play.play(make_hash_model(0))
+    n0, n1 = int(d["sp_lengths"][0]), int(d["sp_lengths"][1])
+    assert [r[2] for r in h] == d["sp_values"][n0:n0 + n1].astype(int).tolist()
+    assert np.array_equal(np.asarray([r[1] for r in h], np.float64).view(np.uint64),
+                          d["sp_policies"][n0:n0 + n1].view(np.uint64))

@@ -175,3 +175,20 @@ def test_oracle_arena_games_match_reference(oracle_lib):
         assert np.array_equal(acts, d["arena_actions"][off:off + n].astype(np.int32)), g
         assert point == d["arena_points"][g], g
         off += n
+
+
+def test_oracle_python_self_play_matches_reference(oracle_lib):
+    """self_play.py play() (Python PV-MCTS self-play, BASELINE configs[0]) after
+    np.random.seed(seed): inputs, float64 policies (bits) and first-player values."""
+    core = oracle_lib
+    d = golden("pvpy.npz")
+    off = 0
+    for g in range(len(d["sp_lengths"])):
+        n = int(d["sp_lengths"][g])
+        r = core.self_play_game_py_hash(int(d["sp_seeds"][g]))
+        sl = slice(off, off + n)
+        assert len(r["values"]) == n, g
+        assert np.array_equal(r["tensors"].astype(np.uint8), d["sp_tensors"][sl]), g
+        assert np.array_equal(r["policies"].view(np.uint64), d["sp_policies"][sl].view(np.uint64)), g
+        assert np.array_equal(r["values"], d["sp_values"][sl]), g
+        off += n

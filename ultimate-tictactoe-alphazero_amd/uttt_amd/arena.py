@@ -131,5 +131,49 @@ def evaluate_network(model0, model1, game_count=50, temperature=1.0, seed_base=0
     return total / game_count, points, actions
 
 
-__all__ = ["ModelEvaluator", "PvMcts", "evaluate_network", "first_player_point", "model_evaluator",
+def first_player_value(state):
+    """self_play.py:20-25."""
+    if state.is_lose():
+        return -1 if state.is_first_player() else 1
+    return 0
+
+
+def self_play_py(model, game_count, seed_base=0, temperature=1.0, evaluate_count=50, batch_size=8, device=None,
+                 make_evaluator=None, progress=None):
+    """self_play.py:66-99 (the Python self-play: pv_mcts.py searches) for game_count games at once.
+    Game g draws from RandomState(seed_base + g) (= play(model) after np.random.seed(seed_base + g)).
+    Returns one history per game: [input (9,9,3) float64, policies (81 Python floats, 0 for
+    illegal actions), value (first_player_value at ply 0, then alternating)]."""
+    import uttt_cpp
+    search = PvMcts(game_count, evaluate_count, device)
+    ev = make_evaluator(model, search.engine) if make_evaluator else model_evaluator(model, game_count)
+    states = [uttt_cpp.State() for _ in range(game_count)]
+    rngs = [np.random.RandomState(seed_base + g) for g in range(game_count)]
+    hist = [[] for _ in range(game_count)]
+    while True:
+        live = [g for g in range(game_count) if not states[g].is_done()]
+        if not live:
+            break
+        vis = search.visits([states[g] for g in live], ev, evaluate_count, batch_size)
+        for g, v in zip(live, vis):
+            st = states[g]
+            legal = st.legal_actions()
+            scores = scores_from_visits(v, temperature)
+            policies = [0] * 81
+            for action, policy in zip(legal, scores):
+                policies[action] = policy
+            x = np.asarray(st.to_input_tensor(), dtype=np.float64).reshape(9, 9, 3)
+            hist[g].append([x, policies, None])
+            states[g] = st.next(int(rngs[g].choice(legal, p=scores)))
+        if progress:
+            progress(game_count - len(live), game_count)
+    for g in range(game_count):
+        value = first_player_value(states[g])
+        for rec in hist[g]:
+            rec[2] = value
+            value = -value
+    return hist
+
+
+__all__ = ["ModelEvaluator", "first_player_value", "self_play_py", "PvMcts", "evaluate_network", "first_player_point", "model_evaluator",
            "scores_from_visits"]
