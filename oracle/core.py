@@ -215,6 +215,26 @@ def pv_mcts_scores_py_hash(state, temperature, evaluate_count=50, batch_size=8, 
     return sc[:n].copy(), vis, st
 
 
+def pv_mcts_scores_py_callback(state, temperature, evaluate_count, batch_size, evaluator):
+    """pv_mcts.py semantics with a Python evaluator(x_nchw (243,) f32) -> (policy[81], value)."""
+
+    def cb(xp, pp, vp, _ctx):
+        x = np.ctypeslib.as_array(xp, shape=(243,)).copy()
+        pol, val = evaluator(x)
+        pol = np.asarray(pol, dtype=np.float32).reshape(-1)
+        for a in range(81):
+            pp[a] = float(pol[a]) if a < pol.size else 0.0
+        vp[0] = float(np.float32(val))
+
+    fn = EVAL_FN(cb)
+    sc = np.zeros(81, np.float64)
+    vi = np.zeros(81, np.int32)
+    st = SearchStats()
+    n = lib().or_pv_mcts_scores_py(ctypes.byref(state), float(temperature), int(evaluate_count), int(batch_size),
+                                   fn, None, sc.ctypes.data_as(F64P), vi.ctypes.data_as(I32P), ctypes.byref(st))
+    return sc[:n].copy(), vi[:n].copy(), st
+
+
 def evaluate_play_hash(seed, salt_first, salt_second, temperature=1.0, evaluate_count=50, batch_size=8):
     """evaluate_network.play after np.random.seed(seed), first player = hash(salt_first).
     Returns (first player's point 0 / 0.5 / 1, actions)."""
