@@ -68,3 +68,64 @@ def test_gloo_gather_two_ranks(tmp_path):
     merged = np.load(tmp_path / "merged.npy")
     single = pack_records(_fake_records(range(n_games)))
     assert np.array_equal(merged, single)
+
+
+# ------------------------------------------------- data-parallel train_network --
+def _history(n, seed):
+    rng = np.random.RandomState(seed)
+    xs = (rng.rand(n, 9, 9, 3) < 0.3).astype(np.float64)
+    ps = rng.rand(n, 81)
+    ps /= ps.sum(axis=1, keepdims=True)
+    vs = rng.randint(-1, 2, size=n)
+    return [[xs[i], ps[i].tolist(), int(vs[i])] for i in range(n)]
+
+
+def _grad_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from uttt_amd import train
+    from uttt_amd.model import random_network
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    model = random_network(0).eval()  # BatchNorm on running statistics: per-sample losses
+    net = train.prepare(model, torch.device("cpu"), sync_bn=False)
+    x, p, v = (torch.from_numpy(a) for a in train.history_arrays(_history(8, 3)))
+    li = train.local_slice(torch.arange(8), rank, world)
+    pp, pv = net(x[li])
+    loss = train.policy_loss_fn(pp, p[li]) + torch.nn.functional.mse_loss(pv, v[li])
+    loss.backward()
+    if rank == 0:
+        torch.save({k: q.grad.clone() for k, q in model.named_parameters()}, os.path.join(out_dir, "g.pt"))
+    # a short train-mode run: replicas stay identical
+    model2 = random_network(1)
+    losses = train.train_network(model2, _history(24, 5), epochs=2, batch_size=8, device=torch.device("cpu"),
+                                 log=None, sync_bn=False)
+    params = {k: q.detach().clone() for k, q in model2.named_parameters()}  # BN running stats stay per
+    torch.save({"sd": params, "losses": losses}, os.path.join(out_dir, f"m{rank}.pt"))  # rank without SyncBN
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_step_equals_single_process(tmp_path):
+    """DDP over 2 gloo ranks, each half of a global batch: the averaged gradients equal the
+    single-process gradients of the whole batch (train_network.py:97-113 loss); a short
+    train-mode run keeps both replicas' parameters identical."""
+    import torch
+    from uttt_amd import train
+    from uttt_amd.model import random_network
+    mp.spawn(_grad_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    model = random_network(0).eval()
+    x, p, v = (torch.from_numpy(a) for a in train.history_arrays(_history(8, 3)))
+    pp, pv = model(x)
+    loss = train.policy_loss_fn(pp, p) + torch.nn.functional.mse_loss(pv, v)
+    loss.backward()
+    g = torch.load(os.path.join(tmp_path, "g.pt"), weights_only=True)
+    for k, q in model.named_parameters():
+        scale = max(q.grad.abs().max().item(), 1e-12)
+        assert (g[k] - q.grad).abs().max().item() <= 1e-4 * scale, k  # f32, different summation order
+    m0 = torch.load(os.path.join(tmp_path, "m0.pt"), weights_only=True)
+    m1 = torch.load(os.path.join(tmp_path, "m1.pt"), weights_only=True)
+    for k in m0["sd"]:
+        assert torch.equal(m0["sd"][k], m1["sd"][k]), k
+    assert m0["losses"] == m1["losses"] and all(np.isfinite(m0["losses"]))

@@ -498,3 +498,20 @@ def test_python_self_play_matches_reference(gpu):
     assert [r[2] for r in h] == d["sp_values"][n0:n0 + n1].astype(int).tolist()
     assert np.array_equal(np.asarray([r[1] for r in h], np.float64).view(np.uint64),
                           d["sp_policies"][n0:n0 + n1].view(np.uint64))
+
+
+def test_train_network_runs_on_gpu(gpu):
+    """uttt_amd.train on the GPU (one process): finite, decreasing loss on a learnable
+    synthetic history; the saved state dict loads back into DualNetwork."""
+    import torch
+    from uttt_amd import train
+    from uttt_amd.model import DualNetwork, random_network
+    rng = np.random.RandomState(0)
+    xs = (rng.rand(256, 9, 9, 3) < 0.3).astype(np.float64)
+    pol = np.zeros((256, 81))
+    pol[np.arange(256), rng.randint(0, 81, 256)] = 1.0
+    hist = [[xs[i], pol[i], int(i % 3) - 1] for i in range(256)]
+    model = random_network(0)
+    losses = train.train_network(model, hist, epochs=6, batch_size=64, device=torch.device("cuda", 0), log=None)
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+    DualNetwork().load_state_dict(model.state_dict())

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""train_network throughput: DualNetwork 128f x16 fp32, batch 128, Adam,
+synthetic history of --samples plies (default 29,000 = 500 games x ~58 plies, the reference's
+self-play output per cycle), data resident in HBM. One JSON line; CPU baseline = the same loop
+on the host for a bounded number of steps.
+usage: python tools/bench_train.py [--samples 29000] [--epochs 2] [--cpu-steps 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "ultimate-tictactoe-alphazero_amd")]
+
+
+def history(n, seed=0):
+    import numpy as np
+    rng = np.random.RandomState(seed)
+    xs = (rng.rand(n, 9, 9, 3) < 0.3).astype(np.float64)
+    ps = rng.rand(n, 81)
+    ps /= ps.sum(axis=1, keepdims=True)
+    vs = rng.randint(-1, 2, size=n)
+    return [[xs[i], ps[i], int(vs[i])] for i in range(n)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--samples", type=int, default=29000)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    from uttt_amd import train
+    from uttt_amd.model import random_network
+    h = history(args.samples)
+    dev = torch.device("cuda", 0)
+    model = random_network(0)
+    train.train_network(model, h[:1024], epochs=1, device=dev, log=None)  # warm-up (MIOpen tuning)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = train.train_network(model, h, epochs=args.epochs, device=dev, log=None)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = args.epochs * -(-args.samples // train.BATCH_SIZE)
+    out = {"metric": "train_network samples/s (DualNetwork 128f x16 fp32, batch 128, Adam)",
+           "value": args.epochs * args.samples / dt, "unit": "samples/s", "n_gpus": 1, "steps": steps,
+           "ms_per_step": 1e3 * dt / steps, "epochs": args.epochs, "losses": losses, "dtype": "f32",
+           "data": f"synthetic history of {args.samples} plies"}
+    if args.cpu_steps:
+        m = random_network(0).train()
+        opt = torch.optim.Adam(m.parameters(), lr=0.001)
+        x, p, v = (torch.from_numpy(a) for a in train.history_arrays(h[:train.BATCH_SIZE]))
+        train.train_step(m, opt, x, p, v)
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            train.train_step(m, opt, x, p, v)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": args.cpu_steps * train.BATCH_SIZE / dt, "unit": "samples/s",
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"{args.cpu_steps} steps of the same loop on the host, {dt:.1f} s"}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
