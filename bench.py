@@ -53,7 +53,8 @@ def nn_macs():
 
 NN_FLOP_PER_STATE = 2 * nn_macs()  # 0.765 GFLOP per evaluated position
 # residual-tower MFMA flops actually executed per board / direct-equivalent flops per state
-TOWER_MFMA_FRACTION = {"fused": 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,          # F(3x3,3x3)
+TOWER_MFMA_FRACTION = {"fused": 3 * 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,      # F(3x3,3x3), 3 f16 products
+                       "fused-f32": 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,      # F(3x3,3x3), f32
                        "fused-wino2": 32 * 25 * 16 * 128 * 128 * 2 / NN_FLOP_PER_STATE}  # F(2x2,3x3)
 
 
@@ -65,7 +66,7 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "fused-wino2", "fused-miopen", "nn", "nn-plain", "hash"],
+    ap.add_argument("--evaluator", choices=["fused", "fused-f32", "fused-wino2", "fused-miopen", "nn", "nn-plain", "hash"],
                     default="fused")
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
@@ -202,7 +203,7 @@ def main():
     if args.evaluator == "hash":
         make_inner = HashEvaluator
     elif args.evaluator.startswith("fused"):
-        conv = {"fused": "wino3", "fused-wino2": "wino", "fused-miopen": "miopen"}[args.evaluator]
+        conv = {"fused": "wino3h", "fused-f32": "wino3", "fused-wino2": "wino", "fused-miopen": "miopen"}[args.evaluator]
         make_inner = lambda eng: FusedNetworkEvaluator(net, eng, conv=conv)  # noqa: E731
     else:
         make_inner = lambda eng: NetworkEvaluator(model, eng.max_trees)  # noqa: E731
@@ -326,9 +327,14 @@ def main():
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
                 "eval_cache_log2": args.cache_log2,
                 "lanes_per_gpu": args.lanes,
-                "evaluator": {"fused": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
-                                       "Winograd F(3x3,3x3) f32-MFMA HIP kernel (csrc/wino3_conv.hip), stem/heads "
-                                       "HIP kernels (csrc/nn_kernels.hip)",
+                "evaluator": {"fused": "DualNetwork 128f x16, f32 activations/accumulation, BN folded; residual-tower "
+                                       "convs as a fused Winograd F(3x3,3x3) HIP kernel whose point GEMMs run as "
+                                       "3-term split-f16 products on the f16 MFMA with f32 accumulation "
+                                       "(csrc/wino3h_conv.hip; f32-level error, 1.4e-6 rel vs f64 per conv, tested "
+                                       "at 1e-5), stem/heads HIP kernels (csrc/nn_kernels.hip)",
+                              "fused-f32": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
+                                           "Winograd F(3x3,3x3) f32-MFMA HIP kernel (csrc/wino3_conv.hip), stem/heads "
+                                           "HIP kernels (csrc/nn_kernels.hip)",
                               "fused-wino2": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
                                              "Winograd F(2x2,3x3) f32-MFMA HIP kernel (csrc/wino_conv.hip), stem/heads "
                                              "HIP kernels (csrc/nn_kernels.hip)",

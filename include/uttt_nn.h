@@ -62,6 +62,21 @@ int uttt_nn_wino3_weights(const float *w, float *u);
 int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, const float *residual, float *y,
                           int32_t n_boards, void *stream);
 
+/* The same F(3x3,3x3) conv with its point GEMMs on the f16 matrix cores at f32-level accuracy
+ * (csrc/wino3h_conv.hip): V and U are each split into f16 hi + lo halves (power-of-two scaled into
+ * f16 range) and M = Vhi Uhi + Vhi Ulo + Vlo Uhi accumulates in f32.
+ * uttt_nn_wino3h_weights: u receives 25*128*128*2 f16 (hi, lo) in the kernel's B-fragment order
+ * U[xi][ci/32][hi|lo][co][(ci%32)/8][ci%8], *u_scale the power of two U was scaled by.
+ * uttt_nn_conv3x3_wino3h: x_amax (required) points at max|x| as u32 float bits (e.g. from
+ * uttt_nn_amax, or the y_amax of the conv that produced x); y_amax (optional) receives
+ * max(y) by atomic max (the caller zeroes it). Other rules as uttt_nn_conv3x3_wino. */
+int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale);
+int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                           const float *residual, float *y, const uint32_t *x_amax, uint32_t *y_amax,
+                           int32_t n_boards, void *stream);
+/* *amax = max(*amax, max |x[i]|) over count floats, as u32 float bits (zero *amax first). */
+int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -292,7 +292,7 @@ def test_fused_evaluator_matches_cpu_fp32(gpu, oracle_lib):
     roots, _ = _random_positions(oracle_lib, 300, seed=13)
     net = random_network(0, "cuda")
     bs = gpu.BatchedSearch(len(roots), 50)
-    for conv in ("wino3", "wino", "miopen"):
+    for conv in ("wino3h", "wino3", "wino", "miopen"):
         _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine, conv=conv))
 
 
@@ -403,6 +403,35 @@ def test_winograd_conv_matches_torch_fp32(gpu):
                 want = torch.relu(ref + (res.double() if res is not None else 0)).float()
                 err = (y - want).abs().max().item()
                 assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, f3, res is None, err)
+
+
+def test_split_f16_winograd_conv_matches_f64(gpu):
+    """The split-f16 F(3x3,3x3) kernel (wino3h) vs an f64 direct conv: within 1e-5 of the
+    output scale (the bar the f32 kernels meet) for ragged board counts (partial last
+    3-board set), inputs spanning 1e-3..1e3 in scale (the power-of-two V scaling), with and
+    without residual; y_amax equals max(y) exactly."""
+    import torch
+    import torch.nn.functional as F
+    from uttt_amd.model import fold_bn, random_network
+    from uttt_amd.nnfast import conv3x3_wino3h, wino3h_weights
+    net = random_network(3)
+    g = torch.Generator().manual_seed(2)
+    for blk_i, n, scale in ((5, 1, 1.0), (5, 2, 1e-3), (0, 4, 1.0), (15, 7, 1e3), (5, 257, 30.0), (9, 1000, 1.0)):
+        blk = net.residual_blocks[blk_i]
+        w, b = fold_bn(blk.conv1, blk.bn1)
+        u, su = wino3h_weights(w)
+        u, w, b = u.cuda(), w.cuda(), b.cuda()
+        x = (torch.relu(torch.randn(n, 81, 128, generator=g)) * scale).cuda()
+        r = (torch.randn(n, 81, 128, generator=g) * scale).cuda()
+        xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
+        ref = F.conv2d(xn.double(), w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
+        for res in (None, r):
+            ya = torch.zeros(1, dtype=torch.int32, device="cuda")
+            y = conv3x3_wino3h(x, u, su, b, res, y_amax=ya)
+            want = torch.relu(ref + (res.double() if res is not None else 0)).float()
+            err = (y - want).abs().max().item()
+            assert err <= 1e-5 * max(1e-30, want.abs().max().item()), (blk_i, n, scale, res is None, err)
+            assert ya.view(torch.float32).item() == y.max().item()
 
 
 # ---------------------------------------------------------------- arena path --

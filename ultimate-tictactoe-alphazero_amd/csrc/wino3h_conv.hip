@@ -1,0 +1,586 @@
+// wino3h_conv.hip — the residual tower's 3x3 convolution (dual_network.py:28-45,
+// 128 -> 128 channels on 9x9 boards) as Winograd F(3x3, 3x3) whose point GEMMs
+// run on the f16 matrix cores with f32-level accuracy (split-f16 products).
+//
+// Same algorithm as wino3_conv.hip (Toom-Cook points {0, 1, -1, 2, inf}: V =
+// B^T d B, M = V (.) U per point, Y = A^T M A), different arithmetic for M:
+// every operand is split into two f16 halves, v = v_hi + v_lo (v_hi = v rounded
+// to f16, v_lo = the remainder rounded to f16: 21-22 significant bits), and
+//
+//   M = V_hi U_hi + V_hi U_lo + V_lo U_hi     (each product exact in f32,
+//                                              accumulated in f32 by the MFMA)
+//
+// i.e. three v_mfma_f32_16x16x32_f16 per 32-channel k-step where the f32 form
+// needs eight v_mfma_f32_16x16x4_f32 per 16 channels: 16.5 against 32 cycles
+// per instruction on gfx950 (tools/diag/mfma_rate.hip), 5.2x fewer MFMA cycles
+// per MAC. The dropped V_lo U_lo term is ~2^-22 relative. To keep both halves
+// in f16's range, V is scaled by a power of two sv chosen from the input's
+// maximum (|V| <= 36 max|x|, so 36 max|x| sv <= 2^15) and U by su from its own
+// maximum (host); the epilogue multiplies by 1/(sv su) (exact). The input
+// maximum comes from the producer: every conv's epilogue (and the caller for
+// the stem output) atomically maxes its output into a u32 slot, so no extra
+// pass is needed. Error against an f64 direct conv: DESIGN.md §5.
+//
+// Workgroup = 8 waves, one set = 3 boards = 27 tiles (rows 27..31 of the two
+// 16-row MFMA blocks are zero padding) x 128 output channels; wave w owns
+// channels 16w..16w+15. Per 32-channel chunk: all waves transform (one tile x
+// channel-pair item per thread, split to f16 hi/lo, into LDS in A-fragment
+// order), barrier, then all waves run the 25 point GEMMs (A from LDS, B from
+// L2 two points ahead) with the previous point's fold (S[a][v] += A^T[a][u] M)
+// spread over the next point's MFMAs; the next chunk's inputs are in flight
+// meanwhile. Y = S A after a set's last chunk, then scale, bias, residual,
+// ReLU, store, output max.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "uttt_nn.h"
+
+namespace uttt {
+void set_error(const char *fmt, ...);
+
+namespace wino3h {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int C = 128;        // channels in and out
+constexpr int NP = 25;        // transform points
+constexpr int KC = 32;        // input channels per chunk (one K=32 MFMA step)
+constexpr int NCH = C / KC;   // chunks per set
+constexpr int BPS = 3;        // boards per set
+constexpr int TS = 9 * BPS;   // tiles per set (27 of the 32 MFMA rows)
+constexpr int PB = 121;       // a board staged zero-padded to 11x11
+constexpr int XP = BPS * PB;  // staged positions
+constexpr int NT = 512;       // threads (8 waves)
+constexpr int NITEM = TS * (KC / 2);             // transform items per chunk (tile, channel pair): 432
+constexpr int VPLANE = 1024;                     // bytes of one (xi, rt, hi|lo) A plane: 4 kq x 16 rows x 16 B
+constexpr int VB = NP * 4 * VPLANE;              // V bytes: [xi][rt][h][kq][row^4kq][8 f16]
+constexpr int XF4 = BPS * 81 * (KC / 4);         // float4s staged per chunk (1944)
+constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (4)
+constexpr float VMAX = 32768.0f;                 // |scaled V|, |scaled U| bound (f16 max 65504)
+
+// Toom-Cook F(3,3) on {0, 1, -1, 2, inf} (as wino3_conv.hip)
+__host__ __device__ constexpr int at(int a, int u) {
+    constexpr int m[3][5] = {{1, 1, 1, 1, 0}, {0, 1, -1, 2, 0}, {0, 1, 1, 4, 1}};
+    return m[a][u];
+}
+
+struct Acc {
+    floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
+};
+
+// fold of point P, as single packed ops o = (row a with A^T[a][u] != 0, pair j),
+// spread over the next point's six MFMA slots
+__host__ __device__ constexpr int n_rows(int u) { return (at(0, u) != 0) + (at(1, u) != 0) + (at(2, u) != 0); }
+__host__ __device__ constexpr int nth_row(int u, int i) {
+    int a = 0;
+    for (; a < 3; ++a)
+        if (at(a, u) != 0 && i-- == 0) break;
+    return a;
+}
+
+template <int P, int O>
+__device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    constexpr int u = P / 5, v = P % 5;
+    if constexpr (O < 4 * n_rows(u)) {
+        constexpr int a = nth_row(u, O / 4), j = O % 4, K = at(a, u);
+        if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        else if constexpr (K == -1)
+            asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        else if constexpr (K == 2) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k2));
+        else asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k4));
+    }
+}
+
+constexpr int NSLOT = 6;  // MFMAs per point
+template <int P, int SL, int O = 0>
+__device__ __forceinline__ void fold_slot(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    constexpr int nops = 4 * n_rows(P / 5);
+    if constexpr (O < nops) {
+        if constexpr (O * NSLOT / nops == SL) fold_op<P, O>(S, m, k2, k4);
+        fold_slot<P, SL, O + 1>(S, m, k2, k4);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void fold_all(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    fold_slot<P, 0>(S, m, k2, k4);
+    fold_slot<P, 1>(S, m, k2, k4);
+    fold_slot<P, 2>(S, m, k2, k4);
+    fold_slot<P, 3>(S, m, k2, k4);
+    fold_slot<P, 4>(S, m, k2, k4);
+    fold_slot<P, 5>(S, m, k2, k4);
+}
+
+// B fragments (U hi, U lo) of one point: U[xi][chunk][h][co][kq][8 f16]; each of the
+// two loads reads 1 KB contiguous per wave (hi and lo planes 8 KB apart)
+struct BFrag {
+    halfx8 h, l;
+};
+constexpr int UPLANE = C * 4 * 16;  // bytes of one (xi, chunk, hi|lo) plane
+__device__ __forceinline__ BFrag load_b(rsrc_t u, int xi, int chunk, int voff) {
+    const int soff = (xi * NCH + chunk) * 2 * UPLANE;
+    BFrag b;
+    b.h = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff, soff, 0));
+    b.l = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff + UPLANE, soff, 0));
+    return b;
+}
+template <int XI>
+__device__ __forceinline__ BFrag load_b_ahead(rsrc_t u, int chunk, int voff) {
+    if constexpr (XI < NP) return load_b(u, XI, chunk, voff);
+    else return load_b(u, XI - NP, (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
+}
+
+// A fragments (V hi / lo of both row blocks) of one point
+struct AFrag {
+    halfx8 h0, l0, h1, l1;
+};
+__device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
+    // sv already points at this lane's 16-byte slot within a plane
+    const char *p = sv + xi * 4 * VPLANE;
+    AFrag a;
+    a.h0 = *reinterpret_cast<const halfx8 *>(p);
+    a.l0 = *reinterpret_cast<const halfx8 *>(p + VPLANE);
+    a.h1 = *reinterpret_cast<const halfx8 *>(p + 2 * VPLANE);
+    a.l1 = *reinterpret_cast<const halfx8 *>(p + 3 * VPLANE);
+    return a;
+}
+
+// Point loop, software-pipelined: B two points ahead (L2), A one point ahead (LDS).
+// The fold of point XI-1 is issued among point XI's MFMAs.
+template <int XI, int MODE>
+__device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag &b0, BFrag &b1,
+                                        AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff) {
+    if constexpr (XI <= NP) {
+        floatx2 m[4];
+        if constexpr (XI < NP) {
+            BFrag b2;
+            if constexpr (MODE & 32) {  // diagnostic: no B loads (operands reused, laundered)
+                b2 = b0;
+                asm volatile("" : "+v"(b2.h), "+v"(b2.l));
+            } else {
+                b2 = load_b_ahead<XI + 2>(u, chunk, voff);
+            }
+            AFrag a1;
+            if constexpr (XI + 1 < NP) {
+                if constexpr (MODE & 16) {  // diagnostic: no A loads
+                    a1 = a0;
+                    asm volatile("" : "+v"(a1.h0), "+v"(a1.l0), "+v"(a1.h1), "+v"(a1.l1));
+                } else {
+                    a1 = load_a(sv, XI + 1);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            floatx4 m0 = {}, m1 = {};
+            constexpr bool fold_here = XI > 0 && !(MODE & 64);
+            // small terms first, then the hi x hi product
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h0, b0.l, m0, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 0>(S, mprev, k2, k4);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h1, b0.l, m1, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 1>(S, mprev, k2, k4);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.l0, b0.h, m0, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 2>(S, mprev, k2, k4);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.l1, b0.h, m1, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 3>(S, mprev, k2, k4);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h0, b0.h, m0, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 4>(S, mprev, k2, k4);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h1, b0.h, m1, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 5>(S, mprev, k2, k4);
+            asm volatile("" : "+v"(m0), "+v"(m1));  // keep this point's MFMAs in its own region
+            m[0] = __builtin_shufflevector(m0, m0, 0, 1);
+            m[1] = __builtin_shufflevector(m0, m0, 2, 3);
+            m[2] = __builtin_shufflevector(m1, m1, 0, 1);
+            m[3] = __builtin_shufflevector(m1, m1, 2, 3);
+            b0 = b1;
+            b1 = b2;
+            if constexpr (XI + 1 < NP) a0 = a1;
+        }
+        if constexpr (XI == NP && !(MODE & 64)) fold_all<XI - 1>(S, mprev, k2, k4);  // nothing left to spread it over
+        if constexpr (XI < NP) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mprev[i] = m[i];
+            xi_loop<XI + 1, MODE>(S, sv, u, b0, b1, a0, mprev, k2, k4, chunk, voff);
+        }
+    }
+}
+
+// inputs of chunk `chunk` of the set starting at board b0 -> registers
+__device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restrict__ x, int b0, int n_boards, int chunk,
+                                       int tid) {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+        const int i = tid + k * NT;
+        xr[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (i < XF4) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const int b = b0 + bp / 81;
+            if (b < n_boards)
+                xr[k] = reinterpret_cast<const float4 *>(x + ((size_t)b * 81 + bp % 81) * C + chunk * KC)[q];
+        }
+    }
+}
+
+// registers -> sX[padded position][32 channels], scaled by sv (a power of two: exact)
+__device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&xr)[XPT], float sv, int tid) {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+        const int i = tid + k * NT;
+        if (i < XF4) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const int pos = bp % 81, sp = (bp / 81) * PB + (pos / 9 + 1) * 11 + pos % 9 + 1;
+            float4 v = xr[k];
+            v.x *= sv;
+            v.y *= sv;
+            v.z *= sv;
+            v.w *= sv;
+            reinterpret_cast<float4 *>(sX + sp * KC)[q] = v;
+        }
+    }
+}
+
+// x -> B^T x for one 5-vector (channel pairs), common subexpressions shared
+__device__ __forceinline__ void bt5(const floatx2 (&d)[5], floatx2 (&t)[5]) {
+    const floatx2 two = {2.0f, 2.0f}, mtwo = {-2.0f, -2.0f};
+    const floatx2 e = d[3] - d[2];
+    const floatx2 f = d[1] - d[2];
+    const floatx2 t3 = d[3] - d[1];
+    const floatx2 g = d[0] - d[2];
+    const floatx2 h = d[4] - d[2];
+    t[0] = __builtin_elementwise_fma(two, g, t3);
+    t[1] = __builtin_elementwise_fma(mtwo, d[1], e);
+    t[2] = __builtin_elementwise_fma(two, f, e);
+    t[3] = t3;
+    t[4] = __builtin_elementwise_fma(mtwo, t3, h);
+}
+
+// (v0, v1) -> packed f16 hi (round toward zero) and f16 lo = the remainder
+__device__ __forceinline__ void split(floatx2 v, uint32_t &hi, uint32_t &lo) {
+    const auto h = __builtin_amdgcn_cvt_pkrtz(v.x, v.y);
+    const floatx2 hf = {(float)h[0], (float)h[1]};
+    const floatx2 r = v - hf;
+    const auto l = __builtin_amdgcn_cvt_pkrtz(r.x, r.y);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// V = B^T d B for item it = (tile lt, channel pair p) -> split -> sV in A-fragment order
+__device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it) {
+    if (it >= NITEM) return;
+    const int p = it % (KC / 2), lt = it / (KC / 2);
+    const int lb = lt / 9, tt = lt % 9, ty = tt / 3, tx = tt % 3;
+    const float *xs = sX + (lb * PB + 3 * ty * 11 + 3 * tx) * KC + 2 * p;
+    // rows first (u = d B), one row of d live at a time, then columns (V = B^T u)
+    // (loads one row ahead; fenced so the scheduler does not hoist all 25 of them
+    // next to the fifteen live accumulators)
+    floatx2 uu[5][5];
+    floatx2 d[2][5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) d[0][j] = *reinterpret_cast<const floatx2 *>(xs + j * KC);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        if (i < 4) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[(i + 1) & 1][j] = *reinterpret_cast<const floatx2 *>(xs + ((i + 1) * 11 + j) * KC);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bt5(d[i & 1], uu[i]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // A fragment: lane (row m, kq) holds k = 8kq..8kq+7; channel pair p is k = 2p, 2p+1
+    const int rt = lt >> 4, m = lt & 15, kq = p >> 2, w = p & 3;
+    char *base = sv + rt * 2 * VPLANE + kq * 256 + ((m ^ (4 * kq)) * 16) + 4 * w;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        const floatx2 col[5] = {uu[0][b], uu[1][b], uu[2][b], uu[3][b], uu[4][b]};
+        floatx2 o[5];
+        bt5(col, o);
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+            uint32_t hi, lo;
+            split(o[a], hi, lo);
+            char *q = base + (a * 5 + b) * 4 * VPLANE;
+            *reinterpret_cast<uint32_t *>(q) = hi;
+            *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;
+        }
+    }
+}
+
+// An opaque copy: index math derived from it is recomputed where it is used
+// instead of being hoisted out of the chunk loop into (spilled) registers.
+__device__ __forceinline__ int fresh(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ float pow2_scale(float amax) {
+    // largest power of two s with 36 * amax * s <= 2^15 (1 for 0 / non-finite)
+    const float b = 36.0f * amax;
+    if (!(b > 0.0f) || !(b < 3.0e38f)) return 1.0f;
+    int e;
+    frexpf(b, &e);  // 2^(e-1) <= b < 2^e
+    e = 15 - e;
+    e = e > 100 ? 100 : (e < -100 ? -100 : e);
+    return ldexpf(1.0f, e);
+}
+
+// MODE (timing ablations only; 0 in the product): 1 skip the transform, 2 skip the
+// point GEMMs, 64 skip the fold.
+template <bool RES, int MODE = 0>
+__global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
+                                                    float u_scale, const float *__restrict__ bias,
+                                                    const float *__restrict__ res, float *__restrict__ y,
+                                                    const uint32_t *__restrict__ x_amax, uint32_t *__restrict__ y_amax,
+                                                    int n_boards) {
+    __shared__ __attribute__((aligned(16))) float sX[XP * KC];  // [padded position][channel], border = 0
+    __shared__ __attribute__((aligned(16))) char sV[VB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nsets = (n_boards + BPS - 1) / BPS;
+    if ((int)blockIdx.x >= nsets) return;
+    const int my_sets = (nsets - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = my_sets * NCH;
+    auto set_b0 = [&](int g) { return ((int)blockIdx.x + (g / NCH) * (int)gridDim.x) * BPS; };
+    const int co = wv * 16 + (lane & 15);
+    const float sv_scale = pow2_scale(__builtin_bit_cast(float, *x_amax));
+    const float inv = 1.0f / (sv_scale * u_scale);  // both powers of two: exact
+    const float bb = bias[co];
+
+    Acc S[15];
+#pragma unroll
+    for (int i = 0; i < 15; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+    const floatx2 k2 = {2.0f, 2.0f}, k4 = {4.0f, 4.0f};
+    float4 xr[XPT];
+    // MODE 256 (diagnostic): u holds 8 replicas, workgroup b reads replica b % 8
+    const uint16_t *ub = (MODE & 256) ? u + (size_t)(blockIdx.x % 8) * (NP * C * C * 2) : u;
+    const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(ub), 0, NP * C * C * 4, 0x00020000);
+    const int kq = lane >> 4;
+    const int voff = (co * 4 + kq) * 16;
+    const int c_rot = blockIdx.x % NCH;
+    auto chunk_of = [&](int g) { return (g % NCH + c_rot) % NCH; };
+    const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (4 * kq)) * 16);
+
+    // zero the padding border of sX and the V rows of tiles 27..31 (never written)
+    for (int i = tid; i < XP * KC; i += NT) sX[i] = 0.0f;
+    for (int i = tid; i < VB / 16; i += NT) reinterpret_cast<uint4 *>(sV)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    BFrag b0v = load_b(ur, 0, c_rot, voff), b1v = load_b(ur, 1, c_rot, voff);
+    load_x(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
+    store_x(sX, xr, sv_scale, tid);
+    __syncthreads();
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+        const int c = g % NCH, ch = chunk_of(g);
+        // the next chunk's inputs load during this chunk's transform (registers are
+        // free then; the point loop needs nearly all of them)
+        if (g + 1 < G) load_x(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+        if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid));
+        __syncthreads();
+        if (g + 1 < G) store_x(sX, xr, sv_scale, fresh(tid));
+        if constexpr ((MODE & 3) != 2) {
+            AFrag a0 = load_a(sv_lane, 0);
+            floatx2 mprev[4];
+            xi_loop<0, MODE>(S, sv_lane, ur, b0v, b1v, a0, mprev, k2, k4, ch, voff);
+        }
+        if (c == NCH - 1) {
+            // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is tile 16rt + 4(lane>>4) + r
+            const int bs = set_b0(g);
+            const int el = fresh(lane), eco = wv * 16 + (el & 15);
+            // one output position (a, b) of all 8 tiles at a time, to keep register pressure low
+            float vmax = 0.0f;
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab) {
+                const int a = ab / 3, b = ab % 3;
+                floatx8 acc = {};
+#pragma unroll
+                for (int v = 0; v < 5; ++v) {
+                    if (at(b, v) == 0) continue;
+                    const Acc &q = S[a * 5 + v];
+                    const floatx8 s8 = {q.p[0].x, q.p[0].y, q.p[1].x, q.p[1].y, q.p[2].x, q.p[2].y, q.p[3].x, q.p[3].y};
+                    acc = at(b, v) == 1 ? acc + s8
+                        : at(b, v) == -1 ? acc - s8
+                                         : __builtin_elementwise_fma(floatx8((float)at(b, v)), s8, acc);
+                }
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int lt = 16 * rt + 4 * (el >> 4) + r;
+                        const int board = bs + lt / 9;
+                        if (lt >= TS || board >= n_boards) continue;
+                        const int tt = lt % 9, ty = tt / 3, tx = tt % 3;
+                        const size_t idx = ((size_t)board * 81 + (3 * ty + a) * 9 + 3 * tx + b) * C + eco;
+                        float o = __builtin_fmaf(acc[4 * rt + r], inv, bb);
+                        if (RES) o += res[idx];
+                        o = fmaxf(o, 0.0f);
+                        y[idx] = o;
+                        vmax = fmaxf(vmax, o);
+                    }
+            }
+            if (y_amax) {
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+                if (lane == 0) atomicMax(y_amax, __builtin_bit_cast(uint32_t, vmax));  // v >= 0: bit order = value order
+            }
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+        }
+        __syncthreads();
+    }
+}
+
+// |x| maximum into *amax (u32 float bits; the caller zeroes it first)
+__global__ __launch_bounds__(256) void k_amax(const float *__restrict__ x, int64_t count, uint32_t *__restrict__ amax) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
+        m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(uint32_t, m));
+}
+
+static int grid_size(int n_boards) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+    }
+    const int nsets = (n_boards + BPS - 1) / BPS;
+    return nsets < cus ? nsets : cus;
+}
+
+}  // namespace wino3h
+}  // namespace uttt
+
+using namespace uttt;
+
+extern "C" {
+
+int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale) {
+    // U[xi=(p,q)][ci][co] = (G g G^T)[p][q] in double, scaled by su = 2^k (max |U| su <= 2^15),
+    // split hi = f16(U su) (round to nearest), lo = f16(U su - hi), stored as
+    // U[xi][ci/32][hi|lo][co][(ci%32)/8][ci%8] (the kernel's B-fragment order)
+    if (!w || !u || !u_scale) {
+        set_error("uttt_nn_wino3h_weights: null pointer");
+        return UTTT_ERR_ARG;
+    }
+    static const double G[5][3] = {{0.5, 0, 0},
+                                   {-0.5, -0.5, -0.5},
+                                   {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                   {1.0 / 6, 1.0 / 3, 2.0 / 3},
+                                   {0, 0, 1}};
+    using namespace wino3h;
+    double *U = new double[(size_t)NP * C * C];
+    double umax = 0.0;
+    for (int co = 0; co < C; ++co)
+        for (int ci = 0; ci < C; ++ci) {
+            const float *g = w + ((size_t)co * C + ci) * 9;
+            double tg[5][3];
+            for (int p = 0; p < 5; ++p)
+                for (int k = 0; k < 3; ++k)
+                    tg[p][k] = G[p][0] * g[0 * 3 + k] + G[p][1] * g[1 * 3 + k] + G[p][2] * g[2 * 3 + k];
+            for (int p = 0; p < 5; ++p)
+                for (int q = 0; q < 5; ++q) {
+                    const double v = tg[p][0] * G[q][0] + tg[p][1] * G[q][1] + tg[p][2] * G[q][2];
+                    U[((size_t)(p * 5 + q) * C + ci) * C + co] = v;
+                    umax = fabs(v) > umax ? fabs(v) : umax;
+                }
+        }
+    if (!std::isfinite(umax)) {
+        delete[] U;
+        set_error("uttt_nn_wino3h_weights: non-finite weights");
+        return UTTT_ERR_ARG;
+    }
+    int e = 0;
+    if (umax > 0.0) {
+        frexp(umax, &e);  // 2^(e-1) <= umax < 2^e
+        e = 15 - e;
+    }
+    const double su = ldexp(1.0, e);
+    for (int xi = 0; xi < NP; ++xi)
+        for (int ci = 0; ci < C; ++ci)
+            for (int co = 0; co < C; ++co) {
+                const double v = U[((size_t)xi * C + ci) * C + co] * su;
+                const _Float16 hi = (_Float16)v;
+                const _Float16 lo = (_Float16)(v - (double)hi);
+                const size_t o = ((((size_t)xi * NCH + ci / KC) * 2 * C + co) * 4 + (ci % KC) / 8) * 8 + ci % 8;
+                u[o] = __builtin_bit_cast(uint16_t, hi);
+                u[o + C * 4 * 8] = __builtin_bit_cast(uint16_t, lo);
+            }
+    delete[] U;
+    *u_scale = (float)su;
+    return UTTT_OK;
+}
+
+int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *residual,
+                           float *y, const uint32_t *x_amax, uint32_t *y_amax, int32_t n_boards, void *stream) {
+    if (!x || !u || !bias || !y || !x_amax || n_boards < 0 || x == y || (residual && residual == y) ||
+        !(u_scale > 0.0f)) {
+        set_error("uttt_nn_conv3x3_wino3h: bad arguments (x_amax required; output must not alias input or residual)");
+        return UTTT_ERR_ARG;
+    }
+    if (n_boards == 0) return UTTT_OK;
+    const dim3 grid(wino3h::grid_size(n_boards));
+    if (residual)
+        hipLaunchKernelGGL(wino3h::k_wino3h_conv<true>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
+                           bias, residual, y, x_amax, y_amax, n_boards);
+    else
+        hipLaunchKernelGGL(wino3h::k_wino3h_conv<false>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
+                           bias, nullptr, y, x_amax, y_amax, n_boards);
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) {
+        set_error("k_wino3h_conv launch: %s", hipGetErrorString(r));
+        return UTTT_ERR_HIP;
+    }
+    return UTTT_OK;
+}
+
+int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream) {
+    if (!x || !amax || count < 0) {
+        set_error("uttt_nn_amax: bad arguments");
+        return UTTT_ERR_ARG;
+    }
+    if (count == 0) return UTTT_OK;
+    int64_t blocks = (count + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(wino3h::k_amax, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, count, amax);
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) {
+        set_error("k_amax launch: %s", hipGetErrorString(r));
+        return UTTT_ERR_HIP;
+    }
+    return UTTT_OK;
+}
+
+// Diagnostic (not declared in uttt_nn.h): the same launch with a timing ablation.
+int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
+                              const uint32_t *x_amax, int32_t n_boards, int32_t mode, void *stream) {
+    const dim3 grid(wino3h::grid_size(n_boards));
+    hipStream_t st = (hipStream_t)stream;
+    using namespace wino3h;
+    switch (mode) {
+        case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 16: hipLaunchKernelGGL((k_wino3h_conv<false, 16>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 32: hipLaunchKernelGGL((k_wino3h_conv<false, 32>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 48: hipLaunchKernelGGL((k_wino3h_conv<false, 48>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards);
+    }
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+}  // extern "C"

@@ -2,8 +2,9 @@
 (csrc/nn_kernels.hip, csrc/wino_conv.hip, include/uttt_nn.h):
 
   leaves --k_stem--> act (n,9,9,128 NHWC, relu(conv_input+bn) applied)
-  16 x [ conv3x3 + b1 + ReLU            (conv="wino3": one Winograd F(3x3,3x3) kernel,
-         conv3x3 + b2 + residual + ReLU ]  conv="wino": one Winograd F(2x2,3x3) kernel,
+  16 x [ conv3x3 + b1 + ReLU            (conv="wino3h": Winograd F(3x3,3x3), split-f16 MFMA,
+         conv3x3 + b2 + residual + ReLU ]  conv="wino3": the same on f32 MFMA,
+                                           conv="wino": Winograd F(2x2,3x3), f32 MFMA,
                                            conv="miopen": MIOpen NHWC conv + k_epilogue)
   --k_heads--> policy (n,81) softmax, value (n,)
 
@@ -60,9 +61,9 @@ def _p(t):
 class FusedNetworkEvaluator:
     needs_input = False
 
-    def __init__(self, net, engine, max_batch=None, conv="wino3"):
+    def __init__(self, net, engine, max_batch=None, conv="wino3h"):
         net = net.eval()
-        assert conv in ("wino3", "wino", "miopen")
+        assert conv in ("wino3h", "wino3", "wino", "miopen")
         self.conv = conv
         self.engine = engine
         self.lib = _lib.load()
@@ -80,7 +81,24 @@ class FusedNetworkEvaluator:
                 self.blocks.append((w1.to(dev).contiguous(memory_format=cl), b1.to(dev),
                                     w2.to(dev).contiguous(memory_format=cl), b2.to(dev)))
             self.heads = pack_heads(net, dev)
-            if conv in ("wino", "wino3"):
+            if conv == "wino3h":
+                self.wino = []
+                for b in net.residual_blocks:
+                    pair = []
+                    for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
+                        w, bb = fold_bn(cv, bn)
+                        u, su = wino3h_weights(w)
+                        pair.append((u.to(dev), su, bb.to(dev)))
+                    self.wino.append(tuple(pair))
+                self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
+                # per-forward maxima: slot 0 bounds the stem output (inputs are 0/1 planes:
+                # relu(b + sum of the positive weight rows)), slot i+1 = max of conv i's output
+                nconv = 2 * len(self.wino)
+                self.amax = torch.zeros(nconv + 1, dtype=torch.float32, device=dev)
+                bound = torch.relu(self.stem_b.double().cpu() + self.stem_w.double().cpu().clamp_min(0).sum(0)).max()
+                self.amax[0] = float(bound)
+                self.amax = self.amax.view(torch.int32)
+            elif conv in ("wino", "wino3"):
                 wfn = wino3_weights if conv == "wino3" else wino_weights
                 self.conv_fn = self.lib.uttt_nn_conv3x3_wino3 if conv == "wino3" else self.lib.uttt_nn_conv3x3_wino
                 self.wino = []
@@ -123,6 +141,20 @@ class FusedNetworkEvaluator:
         stream = ctypes.c_void_p(torch.cuda.current_stream(self.engine.device).cuda_stream)
         x, t, y = self.buf
         check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(x)))
+        if self.conv == "wino3h":
+            am = self.amax
+            am[1:].zero_()
+            slot = lambda i: ctypes.c_void_p(am.data_ptr() + 4 * i)  # noqa: E731
+            fn = self.lib.uttt_nn_conv3x3_wino3h
+            for i, ((u1, s1, b1), (u2, s2, b2)) in enumerate(self.wino):
+                check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), slot(2 * i), slot(2 * i + 1), n,
+                         stream))
+                check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), slot(2 * i + 1), slot(2 * i + 2),
+                         n, stream))
+                x, y = y, x
+            check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
+                                         1 if softmax else 0, stream))
+            return self.policy[:n], self.value[:n]
         for u1, b1, u2, b2 in self.wino:
             check(self.conv_fn(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
             check(self.conv_fn(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
@@ -155,6 +187,39 @@ def wino3_weights(w):
     check(lib.uttt_nn_wino3_weights(wc.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                                     u.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
     return torch.from_numpy(u)
+
+
+def wino3h_weights(w):
+    """Folded conv weight (128,128,3,3) -> (U as f16 hi/lo pairs, 25*128*128*2 int16 in kernel order, su):
+    the split-f16 F(3x3,3x3) kernel's weights, scaled by the power of two su (host, double)."""
+    import numpy as np
+    wc = np.ascontiguousarray(w.detach().float().cpu().numpy())
+    u = np.zeros((25 * 128 * 128 * 2,), np.uint16)
+    su = ctypes.c_float(0.0)
+    lib = _lib.load()
+    check(lib.uttt_nn_wino3h_weights(wc.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                     ctypes.c_void_p(u.ctypes.data), ctypes.byref(su)))
+    return torch.from_numpy(u.view(np.int16)), su.value
+
+
+def amax(x, out=None):
+    """max |x| as a (1,) int32 tensor of float bits on x's device (uttt_nn_amax)."""
+    if out is None:
+        out = torch.zeros(1, dtype=torch.int32, device=x.device)
+    check(_lib.load().uttt_nn_amax(_p(x), x.numel(), _p(out), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return out
+
+
+def conv3x3_wino3h(x, u, su, bias, residual=None, y_amax=None):
+    """Test/utility wrapper for the split-f16 F(3x3,3x3) kernel: x (n,81,128) f32 cuda ->
+    relu(conv3x3(x) + bias (+ residual)); u, su from wino3h_weights()."""
+    y = torch.empty_like(x)
+    xa = amax(x)
+    check(_lib.load().uttt_nn_conv3x3_wino3h(_p(x), _p(u), ctypes.c_float(su), _p(bias),
+                                             _p(residual) if residual is not None else None, _p(y), _p(xa),
+                                             _p(y_amax) if y_amax is not None else None, x.shape[0],
+                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    return y
 
 
 def conv3x3_wino(x, u, bias, residual=None, f3=False):
