@@ -47,6 +47,9 @@ def main():
         t3 = timeit(lambda: lib.uttt_nn_conv3x3_wino3(_p(x), _p(u3), _p(b), None, _p(y), n, st))
         th = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y), _p(xa),
                                                       None, n, st))
+        r = torch.randn_like(x)
+        th_res = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(r), _p(y),
+                                                          _p(xa), None, n, st))
         abl = {m: timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y),
                                                                     _p(xa), n, m, st)) for m in (1, 2, 64, 16, 32, 48, 49, 112)}
         xs = x[:min(n, 512)]
@@ -60,7 +63,7 @@ def main():
         u8 = uh.repeat(8)
         abl[256] = timeit(lambda: lib.uttt_diag_wino3h_ablation(_p(x), _p(u8), ctypes.c_float(su), _p(b), _p(y),
                                                                 _p(xa), n, 256, st))
-        rec = {"boards": n, "wino3_f32_us": round(t3, 1), "wino3h_us": round(th, 1),
+        rec = {"boards": n, "wino3_f32_us": round(t3, 1), "wino3h_us": round(th, 1), "wino3h_res_us": round(th_res, 1),
                "speedup": round(t3 / th, 2), "ablation_us": {str(k): round(v, 1) for k, v in abl.items()},
                "direct_equiv_tflops": round(2 * 81 * 128 * 1152 * n / th / 1e6, 1),
                "err_rel_wino3h": (yh.double() - ref).abs().max().item() / sc,

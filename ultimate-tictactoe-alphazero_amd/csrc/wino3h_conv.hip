@@ -62,7 +62,10 @@ constexpr int VPLANE = 1024;                     // bytes of one (xi, rt, hi|lo)
 constexpr int VB = NP * 4 * VPLANE;              // V bytes: [xi][rt][h][kq][row^4kq][8 f16]
 constexpr int XF4 = BPS * 81 * (KC / 4);         // float4s staged per chunk (1944)
 constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (4)
-constexpr float VMAX = 32768.0f;                 // |scaled V|, |scaled U| bound (f16 max 65504)
+constexpr int OS = C + 4;                        // output tile row stride (floats; padding against bank conflicts)
+constexpr int OROWS = (BPS * 81 + 1) / 2;                       // output rows per epilogue half (122)
+constexpr int OITEMS = (OROWS * C / 4 + NT - 1) / NT;            // float4 outputs per thread and half (8)
+static_assert(OROWS * OS * 4 <= VB, "half an output tile must fit in sV");
 
 // Toom-Cook F(3,3) on {0, 1, -1, 2, inf} (as wino3_conv.hip)
 __host__ __device__ constexpr int at(int a, int u) {
@@ -317,6 +320,12 @@ __device__ __forceinline__ int fresh(int v) {
     return v;
 }
 
+// Workgroup barrier for the LDS hand-offs only: unlike __syncthreads() it does not wait
+// for outstanding global loads (the next chunk's inputs) or stores (the epilogue).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ float pow2_scale(float amax) {
     // largest power of two s with 36 * amax * s <= 2^15 (1 for 0 / non-finite)
     const float b = 36.0f * amax;
@@ -336,8 +345,12 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                                                     const float *__restrict__ res, float *__restrict__ y,
                                                     const uint32_t *__restrict__ x_amax, uint32_t *__restrict__ y_amax,
                                                     int n_boards) {
-    __shared__ __attribute__((aligned(16))) float sX[XP * KC];  // [padded position][channel], border = 0
-    __shared__ __attribute__((aligned(16))) char sV[VB];
+    // sX [padded position][channel] (border = 0) then sV; the epilogue's output
+    // tile (half a set at a time) aliases sV once the set's last point GEMMs are done
+    __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
+    float *const sX = reinterpret_cast<float *>(smem);
+    char *const sV = smem + XP * KC * 4;
+    float *const sO = reinterpret_cast<float *>(sV);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nsets = (n_boards + BPS - 1) / BPS;
     if ((int)blockIdx.x >= nsets) return;
@@ -380,7 +393,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         // free then; the point loop needs nearly all of them)
         if (g + 1 < G) load_x(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
         if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid));
-        __syncthreads();
+        lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sv_scale, fresh(tid));
         if constexpr ((MODE & 3) != 2) {
             AFrag a0 = load_a(sv_lane, 0);
@@ -391,8 +404,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is tile 16rt + 4(lane>>4) + r
             const int bs = set_b0(g);
             const int el = fresh(lane), eco = wv * 16 + (el & 15);
-            // one output position (a, b) of all 8 tiles at a time, to keep register pressure low
-            float vmax = 0.0f;
+            floatx8 Y[9];
 #pragma unroll
             for (int ab = 0; ab < 9; ++ab) {
                 const int a = ab / 3, b = ab % 3;
@@ -406,33 +418,72 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                         : at(b, v) == -1 ? acc - s8
                                          : __builtin_elementwise_fma(floatx8((float)at(b, v)), s8, acc);
                 }
+                Y[ab] = acc;
+            }
 #pragma unroll
-                for (int rt = 0; rt < 2; ++rt)
+            for (int i = 0; i < 15; ++i)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int lt = 16 * rt + 4 * (el >> 4) + r;
-                        const int board = bs + lt / 9;
-                        if (lt >= TS || board >= n_boards) continue;
-                        const int tt = lt % 9, ty = tt / 3, tx = tt % 3;
-                        const size_t idx = ((size_t)board * 81 + (3 * ty + a) * 9 + 3 * tx + b) * C + eco;
-                        float o = __builtin_fmaf(acc[4 * rt + r], inv, bb);
-                        if (RES) o += res[idx];
-                        o = fmaxf(o, 0.0f);
-                        y[idx] = o;
-                        vmax = fmaxf(vmax, o);
+                for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+            // The set's outputs are one contiguous block of y, 243 rows of 128 channels.
+            // Half of it at a time goes through LDS (sV, free now) so that (+ residual),
+            // ReLU and the stores run as coalesced float4s over all threads.
+            const int nrow = (n_boards - bs < BPS ? n_boards - bs : BPS) * 81;
+            const size_t gbase = (size_t)bs * 81 * C;
+            float vmax = 0.0f;
+#pragma unroll 1
+            for (int h = 0; h < 2; ++h) {
+                const int r0 = h * OROWS;
+                lds_barrier();  // sV free (h = 0: point GEMMs done; h = 1: first half read out)
+#pragma unroll
+                for (int ab = 0; ab < 9; ++ab)
+#pragma unroll
+                    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int lt = 16 * rt + 4 * (el >> 4) + r;
+                            const int tt = lt % 9, ty = tt / 3, tx = tt % 3;
+                            const int row = (lt / 9) * 81 + (3 * ty + ab / 3) * 9 + 3 * tx + ab % 3 - r0;
+                            if (lt < TS && row >= 0 && row < OROWS)
+                                sO[row * OS + eco] = __builtin_fmaf(Y[ab][4 * rt + r], inv, bb);
+                        }
+                lds_barrier();
+                const int t = fresh(tid);
+                const int rows = (nrow - r0 < OROWS ? nrow - r0 : OROWS);
+                float4 rr[OITEMS];
+                if constexpr (RES) {
+#pragma unroll
+                    for (int k = 0; k < OITEMS; ++k) {
+                        const int it = t + k * NT;
+                        rr[k] = it / (C / 4) < rows ? reinterpret_cast<const float4 *>(res + gbase)[r0 * (C / 4) + it]
+                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
                     }
+                }
+#pragma unroll
+                for (int k = 0; k < OITEMS; ++k) {
+                    const int it = t + k * NT, row = it / (C / 4), q = it % (C / 4);
+                    if (row >= rows) continue;
+                    float4 v = *reinterpret_cast<const float4 *>(sO + row * OS + 4 * q);
+                    if constexpr (RES) {
+                        v.x += rr[k].x;
+                        v.y += rr[k].y;
+                        v.z += rr[k].z;
+                        v.w += rr[k].w;
+                    }
+                    v.x = fmaxf(v.x, 0.0f);
+                    v.y = fmaxf(v.y, 0.0f);
+                    v.z = fmaxf(v.z, 0.0f);
+                    v.w = fmaxf(v.w, 0.0f);
+                    reinterpret_cast<float4 *>(y + gbase)[r0 * (C / 4) + it] = v;
+                    vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                }
             }
             if (y_amax) {
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
                 if (lane == 0) atomicMax(y_amax, __builtin_bit_cast(uint32_t, vmax));  // v >= 0: bit order = value order
             }
-#pragma unroll
-            for (int i = 0; i < 15; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 

@@ -60,6 +60,7 @@ def _p(t):
 
 class FusedNetworkEvaluator:
     needs_input = False
+    AMAX_RING = 64
 
     def __init__(self, net, engine, max_batch=None, conv="wino3h"):
         net = net.eval()
@@ -92,12 +93,18 @@ class FusedNetworkEvaluator:
                     self.wino.append(tuple(pair))
                 self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
                 # per-forward maxima: slot 0 bounds the stem output (inputs are 0/1 planes:
-                # relu(b + sum of the positive weight rows)), slot i+1 = max of conv i's output
+                # relu(b + sum of the positive weight rows)), slot i+1 = max of conv i's output.
+                # Forwards take fresh slots from a ring that is zeroed once per AMAX_RING
+                # forwards: a per-forward fill kernel would wait for a free CU behind the
+                # other lanes' persistent convolutions.
                 nconv = 2 * len(self.wino)
-                self.amax = torch.zeros(nconv + 1, dtype=torch.float32, device=dev)
-                bound = torch.relu(self.stem_b.double().cpu() + self.stem_w.double().cpu().clamp_min(0).sum(0)).max()
-                self.amax[0] = float(bound)
+                self.amax_stride = nconv + 1
+                self.amax = torch.zeros(self.AMAX_RING * self.amax_stride, dtype=torch.float32, device=dev)
+                self.stem_bound = float(torch.relu(self.stem_b.double().cpu() +
+                                                   self.stem_w.double().cpu().clamp_min(0).sum(0)).max())
+                self.amax[::self.amax_stride] = self.stem_bound
                 self.amax = self.amax.view(torch.int32)
+                self.amax_pos = 0
             elif conv in ("wino", "wino3"):
                 wfn = wino3_weights if conv == "wino3" else wino_weights
                 self.conv_fn = self.lib.uttt_nn_conv3x3_wino3 if conv == "wino3" else self.lib.uttt_nn_conv3x3_wino
@@ -142,9 +149,12 @@ class FusedNetworkEvaluator:
         x, t, y = self.buf
         check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(x)))
         if self.conv == "wino3h":
-            am = self.amax
-            am[1:].zero_()
-            slot = lambda i: ctypes.c_void_p(am.data_ptr() + 4 * i)  # noqa: E731
+            if self.amax_pos == self.AMAX_RING:
+                self.amax.view(torch.float32).zero_()[::self.amax_stride] = self.stem_bound
+                self.amax_pos = 0
+            base = self.amax.data_ptr() + 4 * self.amax_stride * self.amax_pos
+            self.amax_pos += 1
+            slot = lambda i: ctypes.c_void_p(base + 4 * i)  # noqa: E731
             fn = self.lib.uttt_nn_conv3x3_wino3h
             for i, ((u1, s1, b1), (u2, s2, b2)) in enumerate(self.wino):
                 check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), slot(2 * i), slot(2 * i + 1), n,
