@@ -17,8 +17,8 @@ extern "C" {
 
 /* Layout of the packed head-weight block (floats), all BN-folded:
  *   policy 1x1 conv W[2][128], b[2]; value 1x1 conv W[128], b[1];
- *   policy FC W[81][162] (input index = plane*81 + position, torch.flatten of NCHW), b[81];
- *   value FC1 W[256][81], b[256]; value FC2 W[256], b[1]. */
+ *   policy FC W^T[162][81] (input-major; input index = plane*81 + position, torch.flatten
+ *   of NCHW), b[81]; value FC1 W^T[81][256], b[256]; value FC2 W[256], b[1]. */
 #define UTTT_HEAD_PCONV_W 0
 #define UTTT_HEAD_PCONV_B (UTTT_HEAD_PCONV_W + 2 * 128)
 #define UTTT_HEAD_VCONV_W (UTTT_HEAD_PCONV_B + 2)

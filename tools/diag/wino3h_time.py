@@ -51,7 +51,7 @@ def main():
         th_res = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(r), _p(y),
                                                           _p(xa), None, n, st))
         abl = {m: timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y),
-                                                                    _p(xa), n, m, st)) for m in (1, 2, 64, 16, 32, 48, 49, 112)}
+                                                                    _p(xa), n, m, st)) for m in [int(v) for v in os.environ.get("MODES", "1,2,64,16,32,48,49,112").split(",")]}
         xs = x[:min(n, 512)]
         ref = F.conv2d(xs.reshape(-1, 9, 9, 128).permute(0, 3, 1, 2).double(), wc.double(), b.double(), padding=1)
         ref = torch.relu(ref).permute(0, 2, 3, 1).reshape(-1, 81, 128)

@@ -6,7 +6,7 @@
 //               conv is a masked sum of 27 weight rows; no NCHW tensor is built.
 //   k_epilogue  relu(conv + b [+ residual]) in one pass (MIOpen computes the bare conv).
 //   k_heads     1x1 convs (128->2, 128->1) + ReLU, policy FC 162->81 + softmax,
-//               value FC 81->256 + ReLU + FC 256->1 + tanh: one workgroup per position.
+//               value FC 81->256 + ReLU + FC 256->1 + tanh: four positions per workgroup.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -26,22 +26,31 @@ namespace nn {
 constexpr int C = 128;  // DN_FILTERS
 
 // out[s][pos][c] = relu(b[c] + sum_{ch,ky,kx} w[ch*9+ky*3+kx][c] * in_ch(R+ky-1, C+kx-1))
-// One workgroup per leaf: the 27x128 weights and, per output position, the
-// 27-bit mask of set input taps go to LDS; then each thread sums the weight
-// rows of the set taps for (position, 4 channels) items and stores float4s.
+// SB leaves per workgroup: the 27x128 weights go to LDS once for all of them, and
+// per (leaf, output position) the 27-bit mask of set input taps; then each thread
+// sums the weight rows of the set taps for (leaf, position, 4 channels) items and
+// stores float4s (a wave covers two positions: little divergence in the tap loop).
+constexpr int SB = 4;
+__device__ __forceinline__ uint32_t bit3(uint32_t w0, uint32_t w1, uint32_t w2, int a) {
+    // bit a of a 81-bit board held in three 27-bit words, without indexing an array
+    // (a dynamically indexed local array lands in scratch memory)
+    const uint32_t w = a < 27 ? w0 : (a < 54 ? w1 : w2);
+    return (w >> (a % 27)) & 1u;
+}
 __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ leaf, const int32_t *__restrict__ tree_of,
                                               int n, const float *__restrict__ w, const float *__restrict__ b,
                                               float *__restrict__ out) {
     __shared__ float4 s_w[27 * (C / 4)];
-    __shared__ uint32_t s_mask[81];
-    const int slot = blockIdx.x;
+    __shared__ uint32_t s_mask[SB * 81];
+    const int s0 = blockIdx.x * SB;
+    const int nb = n - s0 < SB ? n - s0 : SB;
     const int t = threadIdx.x;
     for (int i = t; i < 27 * (C / 4); i += 256) s_w[i] = reinterpret_cast<const float4 *>(w)[i];
-    if (t < 81) {
-        const uttt_state_t s = leaf[tree_of[slot]];
+    for (int i = t; i < nb * 81; i += 256) {
+        const uttt_state_t s = leaf[tree_of[s0 + i / 81]];
         uint32_t lm[3];
         legal_mask(s, lm);
-        const int R = t / 9, Cc = t % 9;
+        const int pos = i % 81, R = pos / 9, Cc = pos % 9;
         uint32_t m = 0u;
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
@@ -50,19 +59,20 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
                 const int r = R + ky - 1, c = Cc + kx - 1;
                 if (r < 0 || r > 8 || c < 0 || c > 8) continue;
                 const int a = action_at(r * 9 + c), tap = ky * 3 + kx;
-                m |= bit_of(s.own, a) << tap;
-                m |= bit_of(s.opp, a) << (9 + tap);
-                m |= bit_of(lm, a) << (18 + tap);
+                m |= bit3(s.own[0], s.own[1], s.own[2], a) << tap;
+                m |= bit3(s.opp[0], s.opp[1], s.opp[2], a) << (9 + tap);
+                m |= bit3(lm[0], lm[1], lm[2], a) << (18 + tap);
             }
-        s_mask[t] = m;
+        s_mask[i] = m;
     }
     __syncthreads();
     constexpr int CG = C / 4;
-    float4 *o = reinterpret_cast<float4 *>(out) + (size_t)slot * 81 * CG;
-    for (int i = t; i < 81 * CG; i += 256) {
-        const int pos = i / CG, cg = i % CG;
-        float4 acc = reinterpret_cast<const float4 *>(b)[cg];
-        for (uint32_t m = s_mask[pos]; m; m &= m - 1u) {
+    float4 *o = reinterpret_cast<float4 *>(out) + (size_t)s0 * 81 * CG;
+    const float4 bias = reinterpret_cast<const float4 *>(b)[t % CG];  // 256 % CG == 0: fixed per thread
+    for (int i = t; i < nb * 81 * CG; i += 256) {
+        const int cg = i % CG;
+        float4 acc = bias;
+        for (uint32_t m = s_mask[i / CG]; m; m &= m - 1u) {
             const float4 wv = s_w[__builtin_ctz(m) * CG + cg];
             acc.x += wv.x;
             acc.y += wv.y;
@@ -103,83 +113,117 @@ __global__ __launch_bounds__(256) void k_epilogue(const float *__restrict__ x, c
     }
 }
 
-// Head weight block (uttt_nn.h UTTT_HEAD_*): folded 1x1 convs then the FC layers.
+// Head weight block (uttt_nn.h UTTT_HEAD_*): folded 1x1 convs, then the FC layers with
+// their weights stored input-major (consecutive threads = consecutive outputs read
+// consecutive floats). HB positions per workgroup share every weight load.
+constexpr int HB = 4;
 __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, const float *__restrict__ hw, int n,
                                                float *__restrict__ policy, float *__restrict__ value, int softmax) {
-    __shared__ float s_act[81 * (C + 1)];  // +1 pad: column reads by position stride
-    __shared__ float s_h[3 * 81];          // relu(1x1 conv): [p0 | p1 | v] x 81 (NCHW flatten order)
-    __shared__ float s_u[256];
-    __shared__ float s_red[256];
-    const int row = blockIdx.x;
-    if (row >= n) return;
-    const int t = threadIdx.x;
-    const float *a = act + (size_t)row * 81 * C;
-    for (int i = t; i < 81 * C / 4; i += 256) {
-        const float4 v = reinterpret_cast<const float4 *>(a)[i];
-        const int pos = (i * 4) / C, c = (i * 4) % C;
-        float *d = s_act + pos * (C + 1) + c;
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
-    }
-    __syncthreads();
-    if (t < 243) {
-        const int o = t / 81, pos = t % 81;  // o: 0,1 policy planes, 2 value plane
-        const float *wv = hw + (o < 2 ? UTTT_HEAD_PCONV_W + o * C : UTTT_HEAD_VCONV_W);
-        const float bo = hw[o < 2 ? UTTT_HEAD_PCONV_B + o : UTTT_HEAD_VCONV_B];
-        const float *x = s_act + pos * (C + 1);
-        float acc = 0.0f;
-        for (int c = 0; c < C; ++c) acc += wv[c] * x[c];
-        s_h[t] = fmaxf(acc + bo, 0.0f);
-    }
-    __syncthreads();
-    // value FC1 (81 -> 256) + ReLU
+    __shared__ float s_h[HB][3 * 81];  // relu(1x1 conv): [p0 | p1 | v] x 81 (NCHW flatten order)
+    __shared__ float s_z[HB][81];      // policy logits
+    __shared__ float s_v[HB][4];       // value FC2 partial sums, one per wave
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int b0 = blockIdx.x * HB;
+    const int nb = n - b0 < HB ? n - b0 : HB;
+    // 1x1 convs (128 -> 2 policy planes, 128 -> 1 value plane) + ReLU: 16 lanes per
+    // (position, board), 8 channels per lane, 16-lane shuffle reduction
     {
-        const float *w1 = hw + UTTT_HEAD_VFC1_W + t * 81;
-        float acc = hw[UTTT_HEAD_VFC1_B + t];
-        for (int j = 0; j < 81; ++j) acc += w1[j] * s_h[162 + j];
-        s_u[t] = fmaxf(acc, 0.0f);
-    }
-    // policy logits (162 -> 81)
-    float z = -INFINITY;
-    if (t < 81) {
-        const float *wp = hw + UTTT_HEAD_PFC_W + t * 162;
-        float acc = hw[UTTT_HEAD_PFC_B + t];
-        for (int j = 0; j < 162; ++j) acc += wp[j] * s_h[j];
-        z = acc;
+        const int g = t & 15;
+        float w0[8], w1[8], w2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            w0[k] = hw[UTTT_HEAD_PCONV_W + 8 * g + k];
+            w1[k] = hw[UTTT_HEAD_PCONV_W + C + 8 * g + k];
+            w2[k] = hw[UTTT_HEAD_VCONV_W + 8 * g + k];
+        }
+        const float c0 = hw[UTTT_HEAD_PCONV_B], c1 = hw[UTTT_HEAD_PCONV_B + 1], c2 = hw[UTTT_HEAD_VCONV_B];
+        for (int i = t >> 4; i < nb * 81; i += 16) {
+            const float4 *src = reinterpret_cast<const float4 *>(act + ((size_t)b0 * 81 + i) * C + 8 * g);
+            const float4 xa = src[0], xb = src[1];
+            const float x[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                a0 += w0[k] * x[k];
+                a1 += w1[k] * x[k];
+                a2 += w2[k] * x[k];
+            }
+#pragma unroll
+            for (int off = 8; off > 0; off >>= 1) {
+                a0 += __shfl_xor(a0, off);
+                a1 += __shfl_xor(a1, off);
+                a2 += __shfl_xor(a2, off);
+            }
+            if (g == 0) {
+                const int bi = i / 81, pos = i % 81;
+                s_h[bi][pos] = fmaxf(a0 + c0, 0.0f);
+                s_h[bi][81 + pos] = fmaxf(a1 + c1, 0.0f);
+                s_h[bi][162 + pos] = fmaxf(a2 + c2, 0.0f);
+            }
+        }
     }
     __syncthreads();
-    // value FC2 (256 -> 1) + tanh: block reduction
-    s_red[t] = hw[UTTT_HEAD_VFC2_W + t] * s_u[t];
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (t < off) s_red[t] += s_red[t + off];
-        __syncthreads();
+    // value FC1 (81 -> 256) + ReLU, thread t = unit t; FC2 (256 -> 1) partial sums per wave
+    {
+        float acc[HB];
+        const float bt = hw[UTTT_HEAD_VFC1_B + t];
+#pragma unroll
+        for (int bi = 0; bi < HB; ++bi) acc[bi] = bt;
+        const float *w1 = hw + UTTT_HEAD_VFC1_W + t;  // W1^T [81][256]
+        for (int j = 0; j < 81; ++j) {
+            const float wj = w1[j * 256];
+#pragma unroll
+            for (int bi = 0; bi < HB; ++bi) acc[bi] += wj * s_h[bi][162 + j];
+        }
+        const float w2 = hw[UTTT_HEAD_VFC2_W + t];
+#pragma unroll
+        for (int bi = 0; bi < HB; ++bi) {
+            float v = w2 * fmaxf(acc[bi], 0.0f);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) s_v[bi][wv] = v;
+        }
     }
-    if (t == 0) value[row] = tanhf(s_red[0] + hw[UTTT_HEAD_VFC2_B]);
-    if (!softmax) {  // logits (tests compare them: the random-init net's softmax is saturated)
-        if (t < 81) policy[(size_t)row * 81 + t] = z;
-        return;
+    // policy FC (162 -> 81): thread t < 81 * 3 = output t % 81 for boards t / 81, + 3, ...
+    if (t < 243) {
+        const int o = t % 81, g = t / 81;
+        float z[(HB + 2) / 3];
+        const float bo = hw[UTTT_HEAD_PFC_B + o];
+#pragma unroll
+        for (int r = 0; r < (HB + 2) / 3; ++r) z[r] = bo;
+        const float *wp = hw + UTTT_HEAD_PFC_W + o;  // Wp^T [162][81]
+        for (int j = 0; j < 162; ++j) {
+            const float wj = wp[j * 81];
+#pragma unroll
+            for (int r = 0; r < (HB + 2) / 3; ++r)
+                if (g + 3 * r < HB) z[r] += wj * s_h[g + 3 * r][j];
+        }
+#pragma unroll
+        for (int r = 0; r < (HB + 2) / 3; ++r)
+            if (g + 3 * r < HB) s_z[g + 3 * r][o] = z[r];
     }
     __syncthreads();
-    // softmax over 81 logits (threads 0..80 hold z; the others -inf)
-    s_red[t] = z;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (t < off) s_red[t] = fmaxf(s_red[t], s_red[t + off]);
-        __syncthreads();
+    if (t < nb) value[b0 + t] = tanhf(((s_v[t][0] + s_v[t][1]) + (s_v[t][2] + s_v[t][3])) + hw[UTTT_HEAD_VFC2_B]);
+    // softmax over the 81 logits of a board: one wave per board, lanes hold z[lane], z[lane + 64]
+    for (int bi = wv; bi < nb; bi += 4) {
+        float *po = policy + (size_t)(b0 + bi) * 81;
+        const bool two = lane + 64 < 81;
+        const float z0 = s_z[bi][lane], z1 = two ? s_z[bi][lane + 64] : -INFINITY;
+        if (!softmax) {  // logits (tests compare them: the random-init net's softmax is saturated)
+            po[lane] = z0;
+            if (two) po[lane + 64] = z1;
+            continue;
+        }
+        float m = fmaxf(z0, z1);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        const float e0 = expf(z0 - m), e1 = two ? expf(z1 - m) : 0.0f;
+        float sum = e0 + e1;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+        po[lane] = e0 / sum;
+        if (two) po[lane + 64] = e1 / sum;
     }
-    const float zmax = s_red[0];
-    __syncthreads();
-    const float e = t < 81 ? expf(z - zmax) : 0.0f;
-    s_red[t] = e;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (t < off) s_red[t] += s_red[t + off];
-        __syncthreads();
-    }
-    if (t < 81) policy[(size_t)row * 81 + t] = e / s_red[0];
 }
 
 }  // namespace nn
@@ -201,7 +245,7 @@ int uttt_nn_stem(uttt_engine_t *e, const float *w, const float *b, float *out) {
         return UTTT_ERR_ARG;
     }
     if (n == 0) return UTTT_OK;
-    hipLaunchKernelGGL(nn::k_stem, dim3(n), dim3(256), 0, st, leaf, tree_of, n, w, b, out);
+    hipLaunchKernelGGL(nn::k_stem, dim3((n + nn::SB - 1) / nn::SB), dim3(256), 0, st, leaf, tree_of, n, w, b, out);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_stem launch: %s", hipGetErrorString(r));
@@ -235,7 +279,7 @@ int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float 
         return UTTT_ERR_ARG;
     }
     if (n == 0) return UTTT_OK;
-    hipLaunchKernelGGL(nn::k_heads, dim3(n), dim3(256), 0, (hipStream_t)stream, act, head_weights, n, policy, value,
+    hipLaunchKernelGGL(nn::k_heads, dim3((n + nn::HB - 1) / nn::HB), dim3(256), 0, (hipStream_t)stream, act, head_weights, n, policy, value,
                        softmax ? 1 : 0);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {

@@ -213,6 +213,7 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
 }
 
 // inputs of chunk `chunk` of the set starting at board b0 -> registers
+template <int MODE>
 __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restrict__ x, int b0, int n_boards, int chunk,
                                        int tid) {
 #pragma unroll
@@ -222,8 +223,14 @@ __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restric
         if (i < XF4) {
             const int q = i % (KC / 4), bp = i / (KC / 4);
             const int b = b0 + bp / 81;
-            if (b < n_boards)
-                xr[k] = reinterpret_cast<const float4 *>(x + ((size_t)b * 81 + bp % 81) * C + chunk * KC)[q];
+            if (b < n_boards) {
+                const float4 *src = reinterpret_cast<const float4 *>(x + ((size_t)b * 81 + bp % 81) * C + chunk * KC) + q;
+                if constexpr (!(MODE & 512)) {
+                    const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4 *>(src));
+                    xr[k] = make_float4(t.x, t.y, t.z, t.w);
+                }
+                else xr[k] = *src;
+            }
         }
     }
 }
@@ -338,7 +345,10 @@ __device__ __forceinline__ float pow2_scale(float amax) {
 }
 
 // MODE (timing ablations only; 0 in the product): 1 skip the transform, 2 skip the
-// point GEMMs, 64 skip the fold.
+// point GEMMs, 64 skip the fold, 512 plain (L2-allocating) activation loads/stores.
+// The product streams activations with nontemporal loads/stores: each is touched once
+// per launch and would otherwise evict U (1.6 MB, re-read per set) from the XCD's L2
+// (-4..6% at bench batch sizes, tools/diag/wino3h_time.py).
 template <bool RES, int MODE = 0>
 __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
                                                     float u_scale, const float *__restrict__ bias,
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     for (int i = tid; i < VB / 16; i += NT) reinterpret_cast<uint4 *>(sV)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     BFrag b0v = load_b(ur, 0, c_rot, voff), b1v = load_b(ur, 1, c_rot, voff);
-    load_x(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
+    load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
     store_x(sX, xr, sv_scale, tid);
     __syncthreads();
 #pragma unroll 1
@@ -391,7 +401,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         const int c = g % NCH, ch = chunk_of(g);
         // the next chunk's inputs load during this chunk's transform (registers are
         // free then; the point loop needs nearly all of them)
-        if (g + 1 < G) load_x(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+        if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
         if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid));
         lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sv_scale, fresh(tid));
@@ -454,8 +464,12 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
 #pragma unroll
                     for (int k = 0; k < OITEMS; ++k) {
                         const int it = t + k * NT;
-                        rr[k] = it / (C / 4) < rows ? reinterpret_cast<const float4 *>(res + gbase)[r0 * (C / 4) + it]
-                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+                        rr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (it / (C / 4) < rows) {
+                            const floatx4 *src = reinterpret_cast<const floatx4 *>(res + gbase) + r0 * (C / 4) + it;
+                            const floatx4 q = (MODE & 512) ? *src : __builtin_nontemporal_load(src);
+                            rr[k] = make_float4(q.x, q.y, q.z, q.w);
+                        }
                     }
                 }
 #pragma unroll
@@ -473,7 +487,10 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                     v.y = fmaxf(v.y, 0.0f);
                     v.z = fmaxf(v.z, 0.0f);
                     v.w = fmaxf(v.w, 0.0f);
-                    reinterpret_cast<float4 *>(y + gbase)[r0 * (C / 4) + it] = v;
+                    if constexpr (!(MODE & 512))
+                        __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w},
+                                                    reinterpret_cast<floatx4 *>(y + gbase) + r0 * (C / 4) + it);
+                    else reinterpret_cast<float4 *>(y + gbase)[r0 * (C / 4) + it] = v;
                     vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
                 }
             }
@@ -628,6 +645,7 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
         case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards);
     }

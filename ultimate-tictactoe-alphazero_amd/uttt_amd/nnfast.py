@@ -44,8 +44,8 @@ def pack_heads(net, device):
     pw, pb = fold_bn(net.policy_conv, net.policy_bn)
     vw, vb = fold_bn(net.value_conv, net.value_bn)
     parts = {"pconv_w": pw.reshape(-1), "pconv_b": pb, "vconv_w": vw.reshape(-1), "vconv_b": vb,
-             "pfc_w": net.policy_fc.weight.reshape(-1), "pfc_b": net.policy_fc.bias,
-             "vfc1_w": net.value_fc1.weight.reshape(-1), "vfc1_b": net.value_fc1.bias,
+             "pfc_w": net.policy_fc.weight.t().reshape(-1), "pfc_b": net.policy_fc.bias,
+             "vfc1_w": net.value_fc1.weight.t().reshape(-1), "vfc1_b": net.value_fc1.bias,
              "vfc2_w": net.value_fc2.weight.reshape(-1), "vfc2_b": net.value_fc2.bias}
     for k, v in parts.items():
         o, n = lay[k]
