@@ -52,6 +52,10 @@ def main():
                                                           _p(xa), None, n, st))
         abl = {m: timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y),
                                                                     _p(xa), n, m, st)) for m in [int(v) for v in os.environ.get("MODES", "1,2,64,16,32,48,49,112").split(",")]}
+        lib.uttt_diag_wino3h_pf.argtypes = lib.uttt_diag_wino3h_ablation.argtypes
+        for pf in [int(v) for v in os.environ.get("PFS", "").split(",") if v]:
+            abl["pf%d" % pf] = timeit(lambda pf=pf: lib.uttt_diag_wino3h_pf(_p(x), _p(uh), ctypes.c_float(su), _p(b),
+                                                                            _p(y), _p(xa), n, pf, st))
         xs = x[:min(n, 512)]
         ref = F.conv2d(xs.reshape(-1, 9, 9, 128).permute(0, 3, 1, 2).double(), wc.double(), b.double(), padding=1)
         ref = torch.relu(ref).permute(0, 2, 3, 1).reshape(-1, 81, 128)

@@ -21,15 +21,17 @@
 // the stem output) atomically maxes its output into a u32 slot, so no extra
 // pass is needed. Error against an f64 direct conv: DESIGN.md §5.
 //
-// Workgroup = 8 waves, one set = 3 boards = 27 tiles (rows 27..31 of the two
-// 16-row MFMA blocks are zero padding) x 128 output channels; wave w owns
+// Workgroup = 8 waves, one set = 3 boards = 27 tiles (tiles 27..31 of the two
+// 16-tile MFMA blocks are zero padding) x 128 output channels; wave w owns
 // channels 16w..16w+15. Per 32-channel chunk: all waves transform (one tile x
-// channel-pair item per thread, split to f16 hi/lo, into LDS in A-fragment
-// order), barrier, then all waves run the 25 point GEMMs (A from LDS, B from
-// L2 two points ahead) with the previous point's fold (S[a][v] += A^T[a][u] M)
-// spread over the next point's MFMAs; the next chunk's inputs are in flight
-// meanwhile. Y = S A after a set's last chunk, then scale, bias, residual,
-// ReLU, store, output max.
+// channel-pair item per thread, split to f16 hi/lo, into LDS in fragment order),
+// barrier, then all waves run the 25 point GEMMs M^T = U^T V^T (U fragments from
+// L2 a few points ahead as the A operand, V from LDS as the B operand, so a lane's
+// four results are four consecutive output channels of one tile) with the previous
+// point's fold (S[a][v] += A^T[a][u] M) spread over the next point's MFMAs; the
+// next chunk's inputs are in flight meanwhile. Y = S A after a set's last chunk,
+// then scale, bias, residual, ReLU, and one 16-byte store per output position
+// straight from registers, output max.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -62,10 +64,6 @@ constexpr int VPLANE = 1024;                     // bytes of one (xi, rt, hi|lo)
 constexpr int VB = NP * 4 * VPLANE;              // V bytes: [xi][rt][h][kq][row^4kq][8 f16]
 constexpr int XF4 = BPS * 81 * (KC / 4);         // float4s staged per chunk (1944)
 constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (4)
-constexpr int OS = C + 4;                        // output tile row stride (floats; padding against bank conflicts)
-constexpr int OROWS = (BPS * 81 + 1) / 2;                       // output rows per epilogue half (122)
-constexpr int OITEMS = (OROWS * C / 4 + NT - 1) / NT;            // float4 outputs per thread and half (8)
-static_assert(OROWS * OS * 4 <= VB, "half an output tile must fit in sV");
 
 // Toom-Cook F(3,3) on {0, 1, -1, 2, inf} (as wino3_conv.hip)
 __host__ __device__ constexpr int at(int a, int u) {
@@ -154,21 +152,22 @@ __device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
     return a;
 }
 
-// Point loop, software-pipelined: B two points ahead (L2), A one point ahead (LDS).
+// Point loop, software-pipelined: B PF points ahead (L2), A one point ahead (LDS).
 // The fold of point XI-1 is issued among point XI's MFMAs.
-template <int XI, int MODE>
-__device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag &b0, BFrag &b1,
+template <int XI, int MODE, int PF>
+__device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag (&bq)[PF],
                                         AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff) {
     if constexpr (XI <= NP) {
         floatx2 m[4];
         if constexpr (XI < NP) {
             BFrag b2;
             if constexpr (MODE & 32) {  // diagnostic: no B loads (operands reused, laundered)
-                b2 = b0;
+                b2 = bq[0];
                 asm volatile("" : "+v"(b2.h), "+v"(b2.l));
             } else {
-                b2 = load_b_ahead<XI + 2>(u, chunk, voff);
+                b2 = load_b_ahead<XI + PF>(u, chunk, voff);
             }
+            const BFrag b0 = bq[0];
             AFrag a1;
             if constexpr (XI + 1 < NP) {
                 if constexpr (MODE & 16) {  // diagnostic: no A loads
@@ -182,32 +181,33 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             floatx4 m0 = {}, m1 = {};
             constexpr bool fold_here = XI > 0 && !(MODE & 64);
             // small terms first, then the hi x hi product
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h0, b0.l, m0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h0, m0, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 0>(S, mprev, k2, k4);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h1, b0.l, m1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h1, m1, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 1>(S, mprev, k2, k4);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.l0, b0.h, m0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l0, m0, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 2>(S, mprev, k2, k4);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.l1, b0.h, m1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l1, m1, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 3>(S, mprev, k2, k4);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h0, b0.h, m0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h0, m0, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 4>(S, mprev, k2, k4);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0.h1, b0.h, m1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 5>(S, mprev, k2, k4);
             asm volatile("" : "+v"(m0), "+v"(m1));  // keep this point's MFMAs in its own region
             m[0] = __builtin_shufflevector(m0, m0, 0, 1);
             m[1] = __builtin_shufflevector(m0, m0, 2, 3);
             m[2] = __builtin_shufflevector(m1, m1, 0, 1);
             m[3] = __builtin_shufflevector(m1, m1, 2, 3);
-            b0 = b1;
-            b1 = b2;
+#pragma unroll
+            for (int i = 0; i + 1 < PF; ++i) bq[i] = bq[i + 1];
+            bq[PF - 1] = b2;
             if constexpr (XI + 1 < NP) a0 = a1;
         }
         if constexpr (XI == NP && !(MODE & 64)) fold_all<XI - 1>(S, mprev, k2, k4);  // nothing left to spread it over
         if constexpr (XI < NP) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) mprev[i] = m[i];
-            xi_loop<XI + 1, MODE>(S, sv, u, b0, b1, a0, mprev, k2, k4, chunk, voff);
+            xi_loop<XI + 1, MODE, PF>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff);
         }
     }
 }
@@ -344,23 +344,26 @@ __device__ __forceinline__ float pow2_scale(float amax) {
     return ldexpf(1.0f, e);
 }
 
+// MODE+4 phase stamps (core clocks, s_memtime) of workgroups 0..63, waves 0 and 4, first 8
+// chunks: per chunk [after load_x issue, after transform, after barrier+store_x, after GEMMs,
+// after epilogue, after closing barrier] relative to the chunk's start.
+__device__ unsigned int g_stamp[64][2][8][6];
+
 // MODE (timing ablations only; 0 in the product): 1 skip the transform, 2 skip the
 // point GEMMs, 64 skip the fold, 512 plain (L2-allocating) activation loads/stores.
 // The product streams activations with nontemporal loads/stores: each is touched once
 // per launch and would otherwise evict U (1.6 MB, re-read per set) from the XCD's L2
 // (-4..6% at bench batch sizes, tools/diag/wino3h_time.py).
-template <bool RES, int MODE = 0>
+template <bool RES, int MODE = 0, int PF = 4>
 __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
                                                     float u_scale, const float *__restrict__ bias,
                                                     const float *__restrict__ res, float *__restrict__ y,
                                                     const uint32_t *__restrict__ x_amax, uint32_t *__restrict__ y_amax,
                                                     int n_boards) {
-    // sX [padded position][channel] (border = 0) then sV; the epilogue's output
-    // tile (half a set at a time) aliases sV once the set's last point GEMMs are done
+    // sX [padded position][channel] (border = 0) then sV
     __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
     float *const sX = reinterpret_cast<float *>(smem);
     char *const sV = smem + XP * KC * 4;
-    float *const sO = reinterpret_cast<float *>(sV);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nsets = (n_boards + BPS - 1) / BPS;
     if ((int)blockIdx.x >= nsets) return;
@@ -370,7 +373,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     const int co = wv * 16 + (lane & 15);
     const float sv_scale = pow2_scale(__builtin_bit_cast(float, *x_amax));
     const float inv = 1.0f / (sv_scale * u_scale);  // both powers of two: exact
-    const float bb = bias[co];
+    const int co4 = wv * 16 + 4 * (lane >> 4);  // the 4 output channels of this lane's MFMA results
+    const floatx4 bb4 = *reinterpret_cast<const floatx4 *>(bias + co4);
 
     Acc S[15];
 #pragma unroll
@@ -392,106 +396,107 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     for (int i = tid; i < XP * KC; i += NT) sX[i] = 0.0f;
     for (int i = tid; i < VB / 16; i += NT) reinterpret_cast<uint4 *>(sV)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    BFrag b0v = load_b(ur, 0, c_rot, voff), b1v = load_b(ur, 1, c_rot, voff);
+    BFrag bq[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, c_rot, voff);
     load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
     store_x(sX, xr, sv_scale, tid);
     __syncthreads();
+    const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
+    auto mark = [&](int g, int k, unsigned long long t0) {
+        if (stamp && g < 8) g_stamp[blockIdx.x][tid >> 8][g][k] = (unsigned int)(__builtin_amdgcn_s_memtime() - t0);
+    };
 #pragma unroll 1
     for (int g = 0; g < G; ++g) {
         const int c = g % NCH, ch = chunk_of(g);
+        const unsigned long long t0 = (MODE & 4) ? __builtin_amdgcn_s_memtime() : 0ull;
         // the next chunk's inputs load during this chunk's transform (registers are
         // free then; the point loop needs nearly all of them)
         if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+        mark(g, 0, t0);
         if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid));
+        mark(g, 1, t0);
         lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sv_scale, fresh(tid));
+        mark(g, 2, t0);
         if constexpr ((MODE & 3) != 2) {
             AFrag a0 = load_a(sv_lane, 0);
             floatx2 mprev[4];
-            xi_loop<0, MODE>(S, sv_lane, ur, b0v, b1v, a0, mprev, k2, k4, ch, voff);
+            xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff);
         }
+        mark(g, 3, t0);
         if (c == NCH - 1) {
-            // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is tile 16rt + 4(lane>>4) + r
+            // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
+            // of tile 16rt + (lane & 15)
             const int bs = set_b0(g);
-            const int el = fresh(lane), eco = wv * 16 + (el & 15);
-            floatx8 Y[9];
+            const int el = fresh(lane);
+            // Straight from registers: the MFMA output puts 4 consecutive channels of one tile
+            // in a lane (U is the A operand), so every output position is one 16-byte store
+            // (+ one 16-byte residual load, issued before Y is formed); no LDS round trip and
+            // no barrier.
+            const int nb_set = n_boards - bs < BPS ? n_boards - bs : BPS;
+            size_t off[2];
+            bool live[2];
 #pragma unroll
-            for (int ab = 0; ab < 9; ++ab) {
-                const int a = ab / 3, b = ab % 3;
-                floatx8 acc = {};
-#pragma unroll
-                for (int v = 0; v < 5; ++v) {
-                    if (at(b, v) == 0) continue;
-                    const Acc &q = S[a * 5 + v];
-                    const floatx8 s8 = {q.p[0].x, q.p[0].y, q.p[1].x, q.p[1].y, q.p[2].x, q.p[2].y, q.p[3].x, q.p[3].y};
-                    acc = at(b, v) == 1 ? acc + s8
-                        : at(b, v) == -1 ? acc - s8
-                                         : __builtin_elementwise_fma(floatx8((float)at(b, v)), s8, acc);
-                }
-                Y[ab] = acc;
+            for (int rt = 0; rt < 2; ++rt) {
+                const int lt = 16 * rt + (el & 15), lb = lt / 9, tt = lt - 9 * lb;
+                live[rt] = lb < nb_set;  // not a padding tile 27..31 or a board past the end
+                off[rt] = ((size_t)(bs + lb) * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4;
             }
-#pragma unroll
-            for (int i = 0; i < 15; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
-            // The set's outputs are one contiguous block of y, 243 rows of 128 channels.
-            // Half of it at a time goes through LDS (sV, free now) so that (+ residual),
-            // ReLU and the stores run as coalesced float4s over all threads.
-            const int nrow = (n_boards - bs < BPS ? n_boards - bs : BPS) * 81;
-            const size_t gbase = (size_t)bs * 81 * C;
             float vmax = 0.0f;
-#pragma unroll 1
-            for (int h = 0; h < 2; ++h) {
-                const int r0 = h * OROWS;
-                lds_barrier();  // sV free (h = 0: point GEMMs done; h = 1: first half read out)
 #pragma unroll
-                for (int ab = 0; ab < 9; ++ab)
-#pragma unroll
-                    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int lt = 16 * rt + 4 * (el >> 4) + r;
-                            const int tt = lt % 9, ty = tt / 3, tx = tt % 3;
-                            const int row = (lt / 9) * 81 + (3 * ty + ab / 3) * 9 + 3 * tx + ab % 3 - r0;
-                            if (lt < TS && row >= 0 && row < OROWS)
-                                sO[row * OS + eco] = __builtin_fmaf(Y[ab][4 * rt + r], inv, bb);
-                        }
-                lds_barrier();
-                const int t = fresh(tid);
-                const int rows = (nrow - r0 < OROWS ? nrow - r0 : OROWS);
-                float4 rr[OITEMS];
+            for (int rt = 0; rt < 2; ++rt) {
+                // tile block rt: residual loads first (in flight while Y is formed)
+                floatx4 rv[9];
                 if constexpr (RES) {
 #pragma unroll
-                    for (int k = 0; k < OITEMS; ++k) {
-                        const int it = t + k * NT;
-                        rr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-                        if (it / (C / 4) < rows) {
-                            const floatx4 *src = reinterpret_cast<const floatx4 *>(res + gbase) + r0 * (C / 4) + it;
-                            const floatx4 q = (MODE & 512) ? *src : __builtin_nontemporal_load(src);
-                            rr[k] = make_float4(q.x, q.y, q.z, q.w);
+                    for (int ab = 0; ab < 9; ++ab) {
+                        rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+                        if (live[rt]) {
+                            const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+                            rv[ab] = (MODE & 512) ? *src : __builtin_nontemporal_load(src);
                         }
                     }
                 }
+                floatx4 Y[9];
 #pragma unroll
-                for (int k = 0; k < OITEMS; ++k) {
-                    const int it = t + k * NT, row = it / (C / 4), q = it % (C / 4);
-                    if (row >= rows) continue;
-                    float4 v = *reinterpret_cast<const float4 *>(sO + row * OS + 4 * q);
-                    if constexpr (RES) {
-                        v.x += rr[k].x;
-                        v.y += rr[k].y;
-                        v.z += rr[k].z;
-                        v.w += rr[k].w;
+                for (int ab = 0; ab < 9; ++ab) {
+                    const int a = ab / 3, b = ab % 3;
+                    floatx4 acc = {};
+#pragma unroll
+                    for (int v = 0; v < 5; ++v) {
+                        if (at(b, v) == 0) continue;
+                        const Acc &q = S[a * 5 + v];
+                        const floatx4 s4 = {q.p[2 * rt].x, q.p[2 * rt].y, q.p[2 * rt + 1].x, q.p[2 * rt + 1].y};
+                        acc = at(b, v) == 1 ? acc + s4
+                            : at(b, v) == -1 ? acc - s4
+                                             : __builtin_elementwise_fma(floatx4((float)at(b, v)), s4, acc);
                     }
-                    v.x = fmaxf(v.x, 0.0f);
-                    v.y = fmaxf(v.y, 0.0f);
-                    v.z = fmaxf(v.z, 0.0f);
-                    v.w = fmaxf(v.w, 0.0f);
-                    if constexpr (!(MODE & 512))
-                        __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w},
-                                                    reinterpret_cast<floatx4 *>(y + gbase) + r0 * (C / 4) + it);
-                    else reinterpret_cast<float4 *>(y + gbase)[r0 * (C / 4) + it] = v;
-                    vmax = fmaxf(vmax, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+                    Y[ab] = acc;
+                }
+#pragma unroll
+                for (int i = 0; i < 15; ++i) {
+                    S[i].p[2 * rt] = floatx2{0.0f, 0.0f};
+                    S[i].p[2 * rt + 1] = floatx2{0.0f, 0.0f};
+                }
+                if (!live[rt]) continue;
+#pragma unroll
+                for (int ab = 0; ab < 9; ++ab) {
+                    floatx4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv, bb4[r]);
+                    if constexpr (RES) v += rv[ab];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.0f);
+                    floatx4 *dst = reinterpret_cast<floatx4 *>(y + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+                    if constexpr (MODE & 8) {  // diagnostic: no output stores (kept live)
+                        asm volatile("" ::"v"(v));
+                    } else if constexpr (!(MODE & 512)) {
+                        __builtin_nontemporal_store(v, dst);
+                    } else {
+                        *dst = v;
+                    }
+                    vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
                 }
             }
             if (y_amax) {
@@ -500,7 +505,9 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                 if (lane == 0) atomicMax(y_amax, __builtin_bit_cast(uint32_t, vmax));  // v >= 0: bit order = value order
             }
         }
+        mark(g, 4, t0);
         lds_barrier();
+        mark(g, 5, t0);
     }
 }
 
@@ -645,9 +652,37 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
         case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 68: hipLaunchKernelGGL((k_wino3h_conv<false, 68>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 116: hipLaunchKernelGGL((k_wino3h_conv<false, 116>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 20: hipLaunchKernelGGL((k_wino3h_conv<false, 20>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
         default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards);
+    }
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+// Diagnostic: MODE-4 phase stamps, out[64][2][8][6] (see g_stamp).
+int uttt_diag_wino3h_stamps(unsigned int *out) {
+    if (!out || hipMemcpyFromSymbol(out, HIP_SYMBOL(wino3h::g_stamp), sizeof(unsigned int) * 64 * 2 * 8 * 6) != hipSuccess)
+        return UTTT_ERR_HIP;
+    return UTTT_OK;
+}
+
+int uttt_diag_wino3h_pf(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
+                        const uint32_t *x_amax, int32_t n_boards, int32_t pf, void *stream) {
+    const dim3 grid(wino3h::grid_size(n_boards));
+    hipStream_t st = (hipStream_t)stream;
+    using namespace wino3h;
+    switch (pf) {
+        case 3: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 6: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 6>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards);
     }
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }
