@@ -408,7 +408,7 @@ def test_winograd_conv_matches_torch_fp32(gpu):
 def test_split_f16_winograd_conv_matches_f64(gpu):
     """The split-f16 F(3x3,3x3) kernel (wino3h) vs an f64 direct conv: within 1e-5 of the
     output scale (the bar the f32 kernels meet) for ragged board counts (partial last
-    3-board set), inputs spanning 1e-3..1e3 in scale (the power-of-two V scaling), with and
+    7-board group), inputs spanning 1e-3..1e3 in scale (the power-of-two V scaling), with and
     without residual; y_amax equals max(y) exactly."""
     import torch
     import torch.nn.functional as F
@@ -416,7 +416,10 @@ def test_split_f16_winograd_conv_matches_f64(gpu):
     from uttt_amd.nnfast import conv3x3_wino3h, wino3h_weights
     net = random_network(3)
     g = torch.Generator().manual_seed(2)
-    for blk_i, n, scale in ((5, 1, 1.0), (5, 2, 1e-3), (0, 4, 1.0), (15, 7, 1e3), (5, 257, 30.0), (9, 1000, 1.0)):
+    # n covers every residue mod 7 (a 7-board group is two 32-tile sets) and multi-group sizes
+    for blk_i, n, scale in ((5, 1, 1.0), (5, 2, 1e-3), (3, 3, 1.0), (0, 4, 1.0), (2, 5, 1.0), (7, 6, 1.0),
+                            (15, 7, 1e3), (1, 8, 1.0), (4, 11, 1.0), (5, 257, 30.0), (9, 1000, 1.0),
+                            (11, 1603, 1.0)):
         blk = net.residual_blocks[blk_i]
         w, b = fold_bn(blk.conv1, blk.bn1)
         u, su = wino3h_weights(w)

@@ -21,9 +21,12 @@
 // the stem output) atomically maxes its output into a u32 slot, so no extra
 // pass is needed. Error against an f64 direct conv: DESIGN.md §5.
 //
-// Workgroup = 8 waves, one set = 3 boards = 27 tiles (tiles 27..31 of the two
-// 16-tile MFMA blocks are zero padding) x 128 output channels; wave w owns
-// channels 16w..16w+15. Per 32-channel chunk: all waves transform (one tile x
+// Workgroup = 8 waves, one set = 32 tile slots x 128 output channels; wave w owns
+// channels 16w..16w+15. The 63 tiles of 7 consecutive boards are two sets (tiles
+// 0-31: boards 0-3; tiles 32-62: boards 3-6), so 63 of 64 MFMA rows carry a tile, and
+// a set's inputs are 4 boards staged per chunk in rows of 10 (one zero column shared
+// by neighbouring rows) under shared zero rows: every 5x5 window reads its zero
+// border from the layout. Per 32-channel chunk: all waves transform (one tile x
 // channel-pair item per thread, split to f16 hi/lo, into LDS in fragment order),
 // barrier, then all waves run the 25 point GEMMs M^T = U^T V^T (U fragments from
 // L2 a few points ahead as the A operand, V from LDS as the B operand, so a lane's
@@ -54,16 +57,25 @@ constexpr int C = 128;        // channels in and out
 constexpr int NP = 25;        // transform points
 constexpr int KC = 32;        // input channels per chunk (one K=32 MFMA step)
 constexpr int NCH = C / KC;   // chunks per set
-constexpr int BPS = 3;        // boards per set
-constexpr int TS = 9 * BPS;   // tiles per set (27 of the 32 MFMA rows)
-constexpr int PB = 121;       // a board staged zero-padded to 11x11
-constexpr int XP = BPS * PB;  // staged positions
+constexpr int GB = 7;         // boards per group: its 63 tiles are two sets of 32 tile slots
+constexpr int TS = 32;        // tile slots per set (two 16-tile MFMA blocks; the group's 64th is empty)
+constexpr int SB = 4;         // boards a set's tiles touch: boards 0-3 or 3-6 of its group
+constexpr int SR = 10;        // staged row stride: one zero column (shared by neighbouring rows) + 9 cells
+constexpr int XP = (SB * 10 + 1) * SR + 1;  // staged positions (411): boards stacked under shared zero rows
 constexpr int NT = 512;       // threads (8 waves)
-constexpr int NITEM = TS * (KC / 2);             // transform items per chunk (tile, channel pair): 432
+constexpr int NITEM = TS * (KC / 2);             // transform items per chunk (tile slot, channel pair): 512
 constexpr int VPLANE = 1024;                     // bytes of one (xi, rt, hi|lo) A plane: 4 kq x 16 rows x 16 B
 constexpr int VB = NP * 4 * VPLANE;              // V bytes: [xi][rt][h][kq][row^4kq][8 f16]
-constexpr int XF4 = BPS * 81 * (KC / 4);         // float4s staged per chunk (1944)
-constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (4)
+constexpr int XF4 = SB * 81 * (KC / 4);          // float4s staged per chunk (2592)
+constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (6)
+static_assert(NITEM == NT, "one transform item per thread");
+static_assert(XP * KC * 4 + VB <= 160 * 1024, "LDS");
+
+// Sets of n boards: two per full group of 7, one or two for a partial last group
+// (the first set of a group covers boards 0-2 and 5 tiles of board 3).
+__host__ __device__ constexpr int n_sets(int n) { return 2 * (n / GB) + (n % GB == 0 ? 0 : (n % GB <= 3 ? 1 : 2)); }
+// Staged position of cell (r, c) of staged board k; r or c = -1 / 9 land on zero pads.
+__host__ __device__ constexpr int spos(int k, int r, int c) { return (10 * k + r + 1) * SR + c + 1; }
 
 // Toom-Cook F(3,3) on {0, 1, -1, 2, inf} (as wino3_conv.hip)
 __host__ __device__ constexpr int at(int a, int u) {
@@ -216,15 +228,16 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
 template <int MODE>
 __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restrict__ x, int b0, int n_boards, int chunk,
                                        int tid) {
+    // the staged boards are consecutive: their positions are one run of rows of x
+    const int rows = (n_boards - b0) * 81;
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
         const int i = tid + k * NT;
         xr[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (i < XF4) {
             const int q = i % (KC / 4), bp = i / (KC / 4);
-            const int b = b0 + bp / 81;
-            if (b < n_boards) {
-                const float4 *src = reinterpret_cast<const float4 *>(x + ((size_t)b * 81 + bp % 81) * C + chunk * KC) + q;
+            if (bp < rows) {
+                const float4 *src = reinterpret_cast<const float4 *>(x + ((size_t)b0 * 81 + bp) * C + chunk * KC) + q;
                 if constexpr (!(MODE & 512)) {
                     const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4 *>(src));
                     xr[k] = make_float4(t.x, t.y, t.z, t.w);
@@ -242,7 +255,7 @@ __device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&x
         const int i = tid + k * NT;
         if (i < XF4) {
             const int q = i % (KC / 4), bp = i / (KC / 4);
-            const int pos = bp % 81, sp = (bp / 81) * PB + (pos / 9 + 1) * 11 + pos % 9 + 1;
+            const int kb = bp / 81, pos = bp - 81 * kb, sp = spos(kb, pos / 9, pos % 9);
             float4 v = xr[k];
             v.x *= sv;
             v.y *= sv;
@@ -278,12 +291,13 @@ __device__ __forceinline__ void split(floatx2 v, uint32_t &hi, uint32_t &lo) {
     lo = __builtin_bit_cast(uint32_t, l);
 }
 
-// V = B^T d B for item it = (tile lt, channel pair p) -> split -> sV in A-fragment order
-__device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it) {
-    if (it >= NITEM) return;
+// V = B^T d B for item it = (tile slot lt, channel pair p) of a set that is half h of its
+// group -> split -> sV in fragment order. Slot 31 of the second half has no tile: it
+// repeats tile 62, whose results the epilogue drops.
+__device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it, int h) {
     const int p = it % (KC / 2), lt = it / (KC / 2);
-    const int lb = lt / 9, tt = lt % 9, ty = tt / 3, tx = tt % 3;
-    const float *xs = sX + (lb * PB + 3 * ty * 11 + 3 * tx) * KC + 2 * p;
+    const int gt = min(32 * h + lt, GB * 9 - 1), gb = gt / 9, tt = gt - 9 * gb, ty = tt / 3, tx = tt % 3;
+    const float *xs = sX + spos(gb - 3 * h, 3 * ty - 1, 3 * tx - 1) * KC + 2 * p;
     // rows first (u = d B), one row of d live at a time, then columns (V = B^T u)
     // (loads one row ahead; fenced so the scheduler does not hoist all 25 of them
     // next to the fifteen live accumulators)
@@ -295,7 +309,7 @@ __device__ __forceinline__ void transform(char *__restrict__ sv, const float *__
     for (int i = 0; i < 5; ++i) {
         if (i < 4) {
 #pragma unroll
-            for (int j = 0; j < 5; ++j) d[(i + 1) & 1][j] = *reinterpret_cast<const floatx2 *>(xs + ((i + 1) * 11 + j) * KC);
+            for (int j = 0; j < 5; ++j) d[(i + 1) & 1][j] = *reinterpret_cast<const floatx2 *>(xs + ((i + 1) * SR + j) * KC);
         }
         __builtin_amdgcn_sched_barrier(0);
         bt5(d[i & 1], uu[i]);
@@ -354,7 +368,7 @@ __device__ unsigned int g_stamp[64][2][8][6];
 // The product streams activations with nontemporal loads/stores: each is touched once
 // per launch and would otherwise evict U (1.6 MB, re-read per set) from the XCD's L2
 // (-4..6% at bench batch sizes, tools/diag/wino3h_time.py).
-template <bool RES, int MODE = 0, int PF = 4>
+template <bool RES, int MODE = 0, int PF = 3>
 __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
                                                     float u_scale, const float *__restrict__ bias,
                                                     const float *__restrict__ res, float *__restrict__ y,
@@ -365,11 +379,12 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     float *const sX = reinterpret_cast<float *>(smem);
     char *const sV = smem + XP * KC * 4;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nsets = (n_boards + BPS - 1) / BPS;
+    const int nsets = n_sets(n_boards);
     if ((int)blockIdx.x >= nsets) return;
     const int my_sets = (nsets - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     const int G = my_sets * NCH;
-    auto set_b0 = [&](int g) { return ((int)blockIdx.x + (g / NCH) * (int)gridDim.x) * BPS; };
+    auto set_of = [&](int g) { return (int)blockIdx.x + (g / NCH) * (int)gridDim.x; };
+    auto set_b0 = [&](int g) { const int st = set_of(g); return GB * (st >> 1) + 3 * (st & 1); };  // first staged board
     const int co = wv * 16 + (lane & 15);
     const float sv_scale = pow2_scale(__builtin_bit_cast(float, *x_amax));
     const float inv = 1.0f / (sv_scale * u_scale);  // both powers of two: exact
@@ -392,9 +407,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     auto chunk_of = [&](int g) { return (g % NCH + c_rot) % NCH; };
     const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (4 * kq)) * 16);
 
-    // zero the padding border of sX and the V rows of tiles 27..31 (never written)
+    // zero the pads of sX (never written after this)
     for (int i = tid; i < XP * KC; i += NT) sX[i] = 0.0f;
-    for (int i = tid; i < VB / 16; i += NT) reinterpret_cast<uint4 *>(sV)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     BFrag bq[PF];
 #pragma unroll
@@ -414,7 +428,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         // free then; the point loop needs nearly all of them)
         if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
         mark(g, 0, t0);
-        if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid));
+        if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid), set_of(g) & 1);
         mark(g, 1, t0);
         lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sv_scale, fresh(tid));
@@ -427,21 +441,21 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         mark(g, 3, t0);
         if (c == NCH - 1) {
             // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
-            // of tile 16rt + (lane & 15)
-            const int bs = set_b0(g);
+            // of tile slot 16rt + (lane & 15)
+            const int st = set_of(g), grp = st >> 1, h = st & 1;
             const int el = fresh(lane);
             // Straight from registers: the MFMA output puts 4 consecutive channels of one tile
             // in a lane (U is the A operand), so every output position is one 16-byte store
             // (+ one 16-byte residual load, issued before Y is formed); no LDS round trip and
             // no barrier.
-            const int nb_set = n_boards - bs < BPS ? n_boards - bs : BPS;
             size_t off[2];
             bool live[2];
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt) {
-                const int lt = 16 * rt + (el & 15), lb = lt / 9, tt = lt - 9 * lb;
-                live[rt] = lb < nb_set;  // not a padding tile 27..31 or a board past the end
-                off[rt] = ((size_t)(bs + lb) * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4;
+                const int gt = 32 * h + 16 * rt + (el & 15), gb = gt / 9, tt = gt - 9 * gb;
+                const int board = GB * grp + gb;
+                live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
+                off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4;
             }
             float vmax = 0.0f;
 #pragma unroll
@@ -529,7 +543,7 @@ static int grid_size(int n_boards) {
             cus <= 0)
             cus = 256;
     }
-    const int nsets = (n_boards + BPS - 1) / BPS;
+    const int nsets = n_sets(n_boards);
     return nsets < cus ? nsets : cus;
 }
 
