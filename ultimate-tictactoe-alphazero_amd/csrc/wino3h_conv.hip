@@ -292,16 +292,15 @@ __device__ __forceinline__ void split(floatx2 v, uint32_t &hi, uint32_t &lo) {
 }
 
 // V = B^T d B for item it = (tile slot lt, channel pair p) of a set that is half h of its
-// group -> split -> sV in fragment order. Slot 31 of the second half has no tile: it
-// repeats tile 62, whose results the epilogue drops.
-__device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it, int h) {
+// group -> split -> sV in fragment order, in two halves: transform_rows (u = d B; reads sX
+// only) and transform_cols (V = B^T u, split, LDS stores into sV). Slot 31 of the second half has no tile: it repeats tile 62, whose
+// results the epilogue drops.
+__device__ __forceinline__ void transform_rows(floatx2 (&uu)[5][5], const float *__restrict__ sX, int it, int h) {
     const int p = it % (KC / 2), lt = it / (KC / 2);
     const int gt = min(32 * h + lt, GB * 9 - 1), gb = gt / 9, tt = gt - 9 * gb, ty = tt / 3, tx = tt % 3;
     const float *xs = sX + spos(gb - 3 * h, 3 * ty - 1, 3 * tx - 1) * KC + 2 * p;
-    // rows first (u = d B), one row of d live at a time, then columns (V = B^T u)
-    // (loads one row ahead; fenced so the scheduler does not hoist all 25 of them
-    // next to the fifteen live accumulators)
-    floatx2 uu[5][5];
+    // one row of d live at a time (loads one row ahead; fenced so the scheduler does not
+    // hoist all 25 of them next to the fifteen live accumulators)
     floatx2 d[2][5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) d[0][j] = *reinterpret_cast<const floatx2 *>(xs + j * KC);
@@ -315,6 +314,10 @@ __device__ __forceinline__ void transform(char *__restrict__ sv, const float *__
         bt5(d[i & 1], uu[i]);
         __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+__device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floatx2 (&uu)[5][5], int it) {
+    const int p = it % (KC / 2), lt = it / (KC / 2);
     // A fragment: lane (row m, kq) holds k = 8kq..8kq+7; channel pair p is k = 2p, 2p+1
     const int rt = lt >> 4, m = lt & 15, kq = p >> 2, w = p & 3;
     char *base = sv + rt * 2 * VPLANE + kq * 256 + ((m ^ (4 * kq)) * 16) + 4 * w;
@@ -332,6 +335,12 @@ __device__ __forceinline__ void transform(char *__restrict__ sv, const float *__
             *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;
         }
     }
+}
+
+__device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it, int h) {
+    floatx2 uu[5][5];
+    transform_rows(uu, sX, it, h);
+    transform_cols(sv, uu, it);
 }
 
 // An opaque copy: index math derived from it is recomputed where it is used
