@@ -54,8 +54,7 @@ def nn_macs():
 NN_FLOP_PER_STATE = 2 * nn_macs()  # 0.765 GFLOP per evaluated position
 # residual-tower MFMA flops actually executed per board / direct-equivalent flops per state
 TOWER_MFMA_FRACTION = {"fused": 3 * 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,      # F(3x3,3x3), 3 f16 products
-                       "fused-f32": 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,      # F(3x3,3x3), f32
-                       "fused-wino2": 32 * 25 * 16 * 128 * 128 * 2 / NN_FLOP_PER_STATE}  # F(2x2,3x3)
+                       "fused-f32": 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE}      # F(3x3,3x3), f32
 
 
 def parse():
@@ -66,7 +65,7 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "fused-f32", "fused-wino2", "fused-miopen", "nn", "nn-plain", "hash"],
+    ap.add_argument("--evaluator", choices=["fused", "fused-f32", "nn", "nn-plain", "hash"],
                     default="fused")
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
@@ -203,7 +202,7 @@ def main():
     if args.evaluator == "hash":
         make_inner = HashEvaluator
     elif args.evaluator.startswith("fused"):
-        conv = {"fused": "wino3h", "fused-f32": "wino3", "fused-wino2": "wino", "fused-miopen": "miopen"}[args.evaluator]
+        conv = {"fused": "wino3h", "fused-f32": "wino3"}[args.evaluator]
         make_inner = lambda eng: FusedNetworkEvaluator(net, eng, conv=conv)  # noqa: E731
     else:
         make_inner = lambda eng: NetworkEvaluator(model, eng.max_trees)  # noqa: E731
@@ -212,7 +211,7 @@ def main():
     # overlap, so busy time is the union of the intervals), and useful rows
     nn_stats = {"ms": 0.0, "rows": 0, "padded_rows": 0}
     ev_pairs = []
-    pads = args.evaluator in ("nn", "nn-plain", "fused-miopen")
+    pads = args.evaluator in ("nn", "nn-plain")
 
     def make_timed(eng):
         inner = make_inner(eng)
@@ -335,11 +334,6 @@ def main():
                               "fused-f32": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
                                            "Winograd F(3x3,3x3) f32-MFMA HIP kernel (csrc/wino3_conv.hip), stem/heads "
                                            "HIP kernels (csrc/nn_kernels.hip)",
-                              "fused-wino2": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
-                                             "Winograd F(2x2,3x3) f32-MFMA HIP kernel (csrc/wino_conv.hip), stem/heads "
-                                             "HIP kernels (csrc/nn_kernels.hip)",
-                              "fused-miopen": "DualNetwork 128f x16 fp32, BN folded; 3x3 convs MIOpen NHWC, stem/"
-                                              "epilogues/heads as HIP kernels (csrc/nn_kernels.hip)",
                               "nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
                               "nn-plain": "DualNetwork 128f x16 fp32 (PyTorch-ROCm/MIOpen)",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],

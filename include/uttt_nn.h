@@ -1,8 +1,9 @@
 /*
  * uttt_nn.h — C ABI of the DualNetwork leaf-evaluator kernels (dual_network.py:89-121,
  * inference form: BatchNorm folded into each convolution, activations NHWC f32,
- * 128 channels). The 3x3 128->128 convolutions themselves are computed by the
- * caller (MIOpen through PyTorch-ROCm); these kernels replace everything else.
+ * 128 channels): stem, residual-tower convolutions (Winograd F(3x3,3x3) on the
+ * matrix cores) and the two heads. Every kernel computes each board from that
+ * board's inputs only, so outputs do not depend on batch size or composition.
  */
 #ifndef UTTT_NN_H
 #define UTTT_NN_H
@@ -36,28 +37,21 @@ extern "C" {
  * conv_input weight laid out [in_plane*9 + ky*3 + kx][out_channel]
  * (dual_network.py:89-92; planes of uttt_game.cpp:244-280). Engine stream. */
 int uttt_nn_stem(uttt_engine_t *eng, const float *w, const float *b, float *out);
-/* y = relu(x + bias[c] (+ residual)) over rows x channels (NHWC); residual may be NULL
- * (ResidualBlock, dual_network.py:36-45, minus the convolutions). */
-int uttt_nn_epilogue(const float *x, const float *bias, const float *residual, float *y, int64_t rows,
-                     int32_t channels, void *stream);
+/* The same stem from n packed states (any states, e.g. the uttt_cpp.State objects of a
+ * pv_mcts_scores flush), on `stream`. */
+int uttt_nn_stem_states(const uttt_state_t *states, int32_t n, const float *w, const float *b, float *out,
+                        void *stream);
 /* Policy softmax (n,81) (logits if softmax == 0) and tanh value (n) from the final
  * activation (n,81,128) (dual_network.py:106-121). */
 int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float *policy, float *value,
                   int32_t softmax, void *stream);
 
 /* Residual-tower 3x3 conv (128->128, pad 1, 9x9 boards) + bias (+ residual) + ReLU as one
- * Winograd F(2x2,3x3) f32-MFMA kernel (csrc/wino_conv.hip). x, residual, y: [n_boards][81][128]
- * NHWC; y must not alias x or residual. u: 16*128*128 transformed weights U[xi][ci][co] = G g G^T
- * from uttt_nn_wino_weights (host) of a folded conv weight w[128 co][128 ci][3][3], stored in the
- * kernel's B-fragment order U[xi][ci/16][co][ci%2][(ci%16)/2]. */
-int uttt_nn_wino_weights(const float *w, float *u);
-int uttt_nn_conv3x3_wino(const float *x, const float *u, const float *bias, const float *residual, float *y,
-                         int32_t n_boards, void *stream);
-
-/* The same conv as Winograd F(3x3,3x3) (csrc/wino3_conv.hip): a 9x9 board is exactly 3x3 tiles
- * of 3x3 outputs, 25 transform points (Toom-Cook on {0,1,-1,2,inf}). u: 25*128*128 floats,
- * U[xi][ci][co] = G g G^T from uttt_nn_wino3_weights, stored as U[xi][ci/16][co][ci%4][(ci%16)/4].
- * Same argument rules as uttt_nn_conv3x3_wino. */
+ * Winograd F(3x3,3x3) f32-MFMA kernel (csrc/wino3_conv.hip): a 9x9 board is exactly 3x3 tiles
+ * of 3x3 outputs, 25 transform points (Toom-Cook on {0,1,-1,2,inf}). x, residual, y:
+ * [n_boards][81][128] NHWC; y must not alias x or residual. u: 25*128*128 floats,
+ * U[xi][ci][co] = G g G^T from uttt_nn_wino3_weights (host, double) of a folded conv weight
+ * w[128 co][128 ci][3][3], stored as U[xi][ci/16][co][ci%4][(ci%16)/4]. */
 int uttt_nn_wino3_weights(const float *w, float *u);
 int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, const float *residual, float *y,
                           int32_t n_boards, void *stream);
@@ -67,13 +61,17 @@ int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, con
  * f16 range) and M = Vhi Uhi + Vhi Ulo + Vlo Uhi accumulates in f32.
  * uttt_nn_wino3h_weights: u receives 25*128*128*2 f16 (hi, lo) in the kernel's B-fragment order
  * U[xi][ci/32][hi|lo][co][(ci%32)/8][ci%8], *u_scale the power of two U was scaled by.
- * uttt_nn_conv3x3_wino3h: x_amax (required) points at max|x| as u32 float bits (e.g. from
- * uttt_nn_amax, or the y_amax of the conv that produced x); y_amax (optional) receives
- * max(y) by atomic max (the caller zeroes it). Other rules as uttt_nn_conv3x3_wino. */
+ * uttt_nn_conv3x3_wino3h: V is scaled per board, so a board's outputs depend on its own inputs only.
+ * x_amax (required): max|x| as u32 float bits, one per board when x_amax_per_board != 0 (e.g. the
+ * y_amax row of the conv that produced x), else one bound x_amax[0] for every board (the stem).
+ * y_amax (optional): receives max(y) of each board by atomic max (the row must be zero on entry).
+ * amax_clear (optional): the kernel zeroes amax_clear[0 .. clear_count), for a later conv's y_amax;
+ * it must not be x_amax or y_amax. Other rules as uttt_nn_conv3x3_wino3. */
 int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale);
 int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias,
-                           const float *residual, float *y, const uint32_t *x_amax, uint32_t *y_amax,
-                           int32_t n_boards, void *stream);
+                           const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                           uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, int32_t n_boards,
+                           void *stream);
 /* *amax = max(*amax, max |x[i]|) over count floats, as u32 float bits (zero *amax first). */
 int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream);
 

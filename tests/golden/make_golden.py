@@ -11,12 +11,14 @@ Sources of truth used here:
     imported from /root/reference (self-play with numpy's global RNG seeded
     per game), driven by oracle.hashnp.HashModel;
   * the reference's dual_network.py (DualNetwork under torch.manual_seed(0),
-    CPU fp32) for the network I/O fixture;
+    CPU fp32) for the network I/O fixtures: network.npz (the seed-0 net as
+    initialised, saturated) and netcal.npz (the same net with calibrated
+    BatchNorm statistics: O(1) values, spread policies);
   * the reference's pv_mcts.py (Python PV-MCTS, its module constants set per
     case) and evaluate_network.py play() with two salted hash players, numpy's
     global RNG seeded per game (pvpy.npz, the arena path).
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only pvpy]
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only pvpy|netcal]
 """
 import json
 import os
@@ -190,6 +192,51 @@ def gen_network(n_states=24):
     return {"x": x.numpy(), "policy": p.numpy(), "value": v.numpy(), "param_sums": fp, "param_names": names}
 
 
+NETCAL_VFC2_SCALE = 1.0 / 16  # exact power of two
+
+
+def gen_netcal(n_states=256):
+    """A NON-saturated DualNetwork (the seed-0 init saturates: v = -1, one-hot policies) and the
+    reference's own CPU fp32 outputs on it. The net: the reference's DualNetwork under
+    torch.manual_seed(0), BatchNorm running statistics calibrated on 1,024 positions of rules.npz
+    (one train-mode pass with momentum None = the batch statistics, as a trained net would carry),
+    value_fc2.weight scaled by 1/16 (exact). The calibrated buffers are stored, so the network is
+    rebuilt from the seed-0 init + these arrays (uttt_amd.model.calibrated_network)."""
+    sys.path[:0] = [REF]
+    import torch
+    import dual_network  # reference network definition
+    torch.manual_seed(0)
+    net = dual_network.DualNetwork()
+    rules = np.load(os.path.join(HERE, "rules.npz"))
+    n = len(rules["n_legal"])
+    cal = np.random.RandomState(3).choice(n, 1024, replace=False)
+    xc = rules["tensor"][cal].astype(np.float32).reshape(-1, 9, 9, 3).transpose(0, 3, 1, 2)
+    bns = [(name, m) for name, m in net.named_modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    for _, m in bns:
+        m.momentum = None
+        m.reset_running_stats()
+    net.train()
+    with torch.no_grad():
+        net(torch.from_numpy(np.ascontiguousarray(xc)))
+    net.eval()
+    with torch.no_grad():
+        net.value_fc2.weight.mul_(NETCAL_VFC2_SCALE)
+    live = np.nonzero(rules["n_legal"] > 0)[0]
+    rest = np.setdiff1d(live, cal)
+    idx = np.sort(np.random.RandomState(5).choice(rest, n_states, replace=False))
+    x = np.ascontiguousarray(rules["tensor"][idx].astype(np.float32).reshape(-1, 9, 9, 3).transpose(0, 3, 1, 2))
+    with torch.no_grad():
+        p, v = net(torch.from_numpy(x))
+    fp = np.asarray([t.double().sum().item() for t in net.state_dict().values()], np.float64)
+    return {"bn_names": np.asarray([nm for nm, _ in bns]),
+            "bn_mean": np.concatenate([m.running_mean.numpy() for _, m in bns]).astype(np.float32),
+            "bn_var": np.concatenate([m.running_var.numpy() for _, m in bns]).astype(np.float32),
+            "bn_sizes": np.asarray([m.num_features for _, m in bns], np.int32),
+            "vfc2_scale": np.float64(NETCAL_VFC2_SCALE), "rules_index": idx.astype(np.int64),
+            "x": x.astype(np.uint8), "policy": p.numpy(), "value": v.numpy().reshape(-1),
+            "param_sums": fp}
+
+
 PY_CONFIGS = [(50, 8), (50, 1), (30, 3), (10, 2), (1, 1), (7, 100), (64, 64)]
 ARENA_SALTS = (0, 0x5EED5EED12345678)
 
@@ -280,6 +327,12 @@ def gen_pvpy(positions, n_games=8, base_seed=4321):
 
 def main():
     assert ref.available(), "build oracle/_ref first: make -C oracle"
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "netcal":
+        nc = gen_netcal()
+        np.savez_compressed(os.path.join(HERE, "netcal.npz"), **nc)
+        print("netcal:", len(nc["value"]), "states; value range", float(nc["value"].min()), float(nc["value"].max()),
+              "; median max policy", float(np.median(nc["policy"].max(1))))
+        return
     if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "pvpy":
         rules = dict(np.load(os.path.join(HERE, "rules.npz")))
         positions = sample_positions(rules) + [initial(), win_in_one()]
@@ -308,6 +361,9 @@ def main():
     pv = gen_pvpy(positions)
     np.savez_compressed(os.path.join(HERE, "pvpy.npz"), **pv)
     print("pvpy:", len(pv["n"]), "searches;", len(pv["arena_lengths"]), "arena games")
+    nc = gen_netcal()
+    np.savez_compressed(os.path.join(HERE, "netcal.npz"), **nc)
+    print("netcal:", len(nc["value"]), "states")
 
 
 if __name__ == "__main__":

@@ -5,15 +5,17 @@ Evaluators: the device hash evaluator (deterministic, exercises zero /
 subnormal / sparse priors) and the real DualNetwork, whose outputs are
 recorded and replayed into the oracle so search parity is checked
 independently of network numerics."""
+import os
 import random
 
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import GOLDEN, golden
 
 pytestmark = pytest.mark.gpu
 
+NETCAL = os.path.join(GOLDEN, "netcal.npz")
 CONFIGS = [(50, 8), (50, 1), (50, 1024), (400, 8), (10, 2), (30, 3), (1, 1), (7, 100), (64, 64)]
 
 
@@ -235,14 +237,16 @@ def test_network_gpu_matches_cpu_fp32(gpu):
         assert ((z.cpu() - z_cpu).abs() / scale).max().item() <= 1e-4
 
 
-def test_nn_in_the_loop_search_replays_exactly(gpu, oracle_lib):
-    """Engine + real DualNetwork on the GPU; every (input -> output) pair the
-    network produced is replayed into the oracle: visit counts must be equal."""
+@pytest.mark.parametrize("netkind", ["seed0", "calibrated"])
+def test_nn_in_the_loop_search_replays_exactly(gpu, oracle_lib, netkind):
+    """Engine + real DualNetwork (PyTorch-ROCm) on the GPU; every (input -> output) pair the
+    network produced is replayed into the oracle: visit counts must be equal. The
+    calibrated (non-saturated) net gives wide, realistic trees."""
     import torch
-    from uttt_amd.model import random_network
+    from uttt_amd.model import calibrated_network, random_network
     core = oracle_lib
     roots, ostates = _random_positions(core, 64, seed=11)
-    net = random_network(0, "cuda")
+    net = random_network(0, "cuda") if netkind == "seed0" else calibrated_network(NETCAL, "cuda")
     table = {}
 
     class Recording(gpu.NetworkEvaluator):
@@ -284,22 +288,23 @@ def test_full_size_4096x50_properties_and_samples(gpu, oracle_lib):
 
 
 def test_fused_evaluator_matches_cpu_fp32(gpu, oracle_lib):
-    """Stem-from-bitboards + MIOpen NHWC convs + HIP epilogues + HIP heads vs the
-    plain DualNetwork on CPU fp32, on real pending leaves of a search."""
-    import torch
-    from uttt_amd.model import policy_logits, random_network
+    """Stem-from-bitboards + Winograd tower + HIP heads vs the plain DualNetwork on CPU
+    fp32, on real pending leaves of a search, for both tower kernels; the saturated seed-0
+    net (logits checked relative to their scale) and the calibrated one (post-softmax
+    policy and value within 1e-5 absolute)."""
+    from uttt_amd.model import calibrated_network, random_network
     from uttt_amd.nnfast import FusedNetworkEvaluator
     roots, _ = _random_positions(oracle_lib, 300, seed=13)
-    net = random_network(0, "cuda")
     bs = gpu.BatchedSearch(len(roots), 50)
-    for conv in ("wino3h", "wino3", "wino", "miopen"):
-        _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine, conv=conv))
+    for make, sat in ((lambda d: random_network(0, d), True), (lambda d: calibrated_network(NETCAL, d), False)):
+        net = make("cuda")
+        for conv in ("wino3h", "wino3"):
+            _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine, conv=conv), make("cpu"), sat)
 
 
-def _fused_vs_cpu(gpu, bs, roots, fused):
+def _fused_vs_cpu(gpu, bs, roots, fused, cpu, saturated):
     import torch
-    from uttt_amd.model import policy_logits, random_network
-    cpu = random_network(0)
+    from uttt_amd.model import policy_logits
     e = bs.engine
     e.use_stream()
     e.search_begin(roots, 50, 8)
@@ -312,18 +317,22 @@ def _fused_vs_cpu(gpu, bs, roots, fused):
         assert ((z.cpu() - z_cpu).abs() / scale).max().item() <= 1e-4
         p, v2 = fused.forward(n, softmax=True)
         assert torch.allclose(p.sum(dim=1).cpu(), torch.ones(n), atol=1e-5)
+        if not saturated:  # (a saturated softmax turns logit rounding noise into O(1) differences)
+            assert (p.cpu() - torch.softmax(z_cpu, dim=1)).abs().max().item() <= 1e-5
         e.apply(p, v2)
 
 
-def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib):
+@pytest.mark.parametrize("netkind", ["seed0", "calibrated"])
+def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib, netkind):
     """Search with the fused evaluator; its outputs replayed into the oracle give
     the same root visit counts."""
-    from uttt_amd.model import random_network
+    from uttt_amd.model import calibrated_network, random_network
     from uttt_amd.nnfast import FusedNetworkEvaluator
     core = oracle_lib
     roots, ostates = _random_positions(core, 48, seed=17)
     bs = gpu.BatchedSearch(len(roots), 50)
-    fused = FusedNetworkEvaluator(random_network(0, "cuda"), bs.engine)
+    net = random_network(0, "cuda") if netkind == "seed0" else calibrated_network(NETCAL, "cuda")
+    fused = FusedNetworkEvaluator(net, bs.engine)
     table = {}
 
     def recording(x, n):
@@ -342,24 +351,29 @@ def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib):
 
 
 def test_fused_selfplay_lanes_are_bit_identical(gpu):
-    """Self-play with the fused network evaluator: 2 lanes (two engines on two
-    streams, network calls overlapping) give the same records bit for bit as one
-    lane - every kernel computes a board independently of the batch it is in."""
-    from uttt_amd.model import random_network
+    """Self-play with the fused network evaluator on the calibrated (non-saturated) net:
+    1 lane without the evaluation cache, 1 lane with it, and 2 lanes sharing it (two
+    engines on two streams, network calls overlapping) give the same records bit for
+    bit - every kernel computes a board independently of the batch it is in, so cached
+    outputs equal fresh ones."""
+    from uttt_amd.model import calibrated_network
     from uttt_amd.nnfast import FusedNetworkEvaluator
-    net = random_network(0, "cuda")
+    net = calibrated_network(NETCAL, "cuda")
     out = []
-    for lanes in (1, 2):
-        sp = gpu.SelfPlay(16, 50, 8, 1.0, lanes=lanes)
+    for lanes, cache in ((1, 0), (1, 16), (2, 16)):
+        sp = gpu.SelfPlay(16, 50, 8, 1.0, lanes=lanes, cache_log2=cache)
         sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng))
         sp.run(0, 12, 4321)
         out.append(sp.records())
-    a, b = out
-    assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(12))
-    for ra, rb in zip(a, b):
-        assert np.array_equal(ra["actions"], rb["actions"])
-        assert np.array_equal(ra["policies"].view(np.uint64), rb["policies"].view(np.uint64))
-        assert np.array_equal(ra["values"], rb["values"])
+        if cache:
+            assert sp.cache_stats()["hits"] > 0
+    a = out[0]
+    for b in out[1:]:
+        assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(12))
+        for ra, rb in zip(a, b):
+            assert np.array_equal(ra["actions"], rb["actions"])
+            assert np.array_equal(ra["policies"].view(np.uint64), rb["policies"].view(np.uint64))
+            assert np.array_equal(ra["values"], rb["values"])
 
 
 def test_eval_cache_is_exact(gpu, oracle_lib):
@@ -380,16 +394,16 @@ def test_eval_cache_is_exact(gpu, oracle_lib):
 
 
 def test_winograd_conv_matches_torch_fp32(gpu):
-    """The fused Winograd conv (+bias, +residual, ReLU) vs torch fp32 conv2d on the
-    same folded weights, for ragged board counts (tail workgroups)."""
+    """The f32-MFMA F(3x3,3x3) conv (+bias, +residual, ReLU) vs an f64 conv2d on the same
+    folded weights, for ragged board counts (tail workgroups)."""
     import torch
     import torch.nn.functional as F
     from uttt_amd.model import fold_bn, random_network
-    from uttt_amd.nnfast import conv3x3_wino, wino3_weights, wino_weights
+    from uttt_amd.nnfast import conv3x3_wino3, wino3_weights
     net = random_network(3)
     blk = net.residual_blocks[5]
     w, b = fold_bn(blk.conv1, blk.bn1)
-    us = {False: wino_weights(w).cuda(), True: wino3_weights(w).cuda()}
+    u = wino3_weights(w).cuda()
     w, b = w.cuda(), b.cuda()
     g = torch.Generator().manual_seed(1)
     for n in (1, 3, 4, 5, 64, 257, 1000):
@@ -397,19 +411,18 @@ def test_winograd_conv_matches_torch_fp32(gpu):
         r = torch.randn(n, 81, 128, generator=g).cuda()
         xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
         ref = F.conv2d(xn.double(), w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
-        for f3 in (False, True):
-            for res in (None, r):
-                y = conv3x3_wino(x, us[f3], b, res, f3=f3)
-                want = torch.relu(ref + (res.double() if res is not None else 0)).float()
-                err = (y - want).abs().max().item()
-                assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, f3, res is None, err)
+        for res in (None, r):
+            y = conv3x3_wino3(x, u, b, res)
+            want = torch.relu(ref + (res.double() if res is not None else 0)).float()
+            err = (y - want).abs().max().item()
+            assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, res is None, err)
 
 
 def test_split_f16_winograd_conv_matches_f64(gpu):
-    """The split-f16 F(3x3,3x3) kernel (wino3h) vs an f64 direct conv: within 1e-5 of the
-    output scale (the bar the f32 kernels meet) for ragged board counts (partial last
-    7-board group), inputs spanning 1e-3..1e3 in scale (the power-of-two V scaling), with and
-    without residual; y_amax equals max(y) exactly."""
+    """The split-f16 F(3x3,3x3) kernel (wino3h) vs an f64 direct conv: within 1e-5 of each
+    board's output scale (the bar the f32 kernels meet) for ragged board counts (partial last
+    7-board group), inputs spanning 1e-3..1e3 in scale (the per-board power-of-two V scaling),
+    with and without residual; the per-board y_amax row equals each board's max(y) exactly."""
     import torch
     import torch.nn.functional as F
     from uttt_amd.model import fold_bn, random_network
@@ -429,12 +442,118 @@ def test_split_f16_winograd_conv_matches_f64(gpu):
         xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
         ref = F.conv2d(xn.double(), w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
         for res in (None, r):
-            ya = torch.zeros(1, dtype=torch.int32, device="cuda")
+            ya = torch.zeros(n, dtype=torch.int32, device="cuda")
             y = conv3x3_wino3h(x, u, su, b, res, y_amax=ya)
             want = torch.relu(ref + (res.double() if res is not None else 0)).float()
-            err = (y - want).abs().max().item()
-            assert err <= 1e-5 * max(1e-30, want.abs().max().item()), (blk_i, n, scale, res is None, err)
-            assert ya.view(torch.float32).item() == y.max().item()
+            err = (y - want).abs().reshape(n, -1).amax(dim=1)
+            bscale = want.abs().reshape(n, -1).amax(dim=1).clamp_min(1e-30)
+            assert (err / bscale).max().item() <= 1e-5, (blk_i, n, scale, res is None, (err / bscale).max().item())
+            assert torch.equal(ya.view(torch.float32), y.reshape(n, -1).amax(dim=1))
+
+
+def _rules_states(idx):
+    """Packed engine states of rules.npz rows."""
+    from uttt_amd._lib import STATE_DTYPE
+    r = golden("rules.npz")
+    out = np.zeros(len(idx), STATE_DTYPE)
+    for j, i in enumerate(idx):
+        p = r["pieces"][i].astype(np.uint32)
+        e = r["enemy"][i].astype(np.uint32)
+        for a in range(81):
+            out["own"][j, a // 27] |= p[a] << (a % 27)
+            out["opp"][j, a // 27] |= e[a] << (a % 27)
+        out["mains"][j] = sum(int(r["main_p"][i][b]) << b for b in range(9)) | \
+            sum(int(r["main_e"][i][b]) << (16 + b) for b in range(9))
+        out["active"][j] = r["active"][i]
+    return out
+
+
+def test_networks_match_reference_on_calibrated_net(gpu):
+    """North-star network bound on a NON-saturated net (tests/golden/netcal.npz: the
+    reference's own dual_network.py on CPU fp32, calibrated BatchNorm statistics, values in
+    about [-0.9, 0.25], median max policy 0.13): every GPU evaluator - the fused HIP
+    evaluator with the split-f16 tower (default) and with the f32-MFMA tower, and the
+    PyTorch-ROCm DualNetwork plain and BN-folded - within 1e-5 absolute on the value and
+    on every post-softmax policy entry."""
+    import torch
+    from uttt_amd.model import FoldedDualNetwork, calibrated_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    d = golden("netcal.npz")
+    states = _rules_states(d["rules_index"])
+    x = torch.from_numpy(d["x"].astype(np.float32))
+    # the fixture's inputs are these states' tensors (uttt_game.cpp:244-280, NCHW)
+    r = golden("rules.npz")
+    hwc = r["tensor"][d["rules_index"]].reshape(-1, 9, 9, 3).transpose(0, 3, 1, 2)
+    assert np.array_equal(hwc, d["x"])
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    net = calibrated_network(NETCAL, "cuda")
+    outs = {}
+    for conv in ("wino3h", "wino3"):
+        fe = FusedNetworkEvaluator(net, None, max_batch=len(states), conv=conv)
+        p, v = fe.forward_states(states)
+        outs["fused-" + conv] = (p.cpu().numpy(), v.cpu().numpy())
+    with torch.no_grad():
+        p, v = net(x.cuda())
+        outs["torch"] = (p.cpu().numpy(), v.cpu().numpy().reshape(-1))
+        p, v = FoldedDualNetwork(net).to("cuda")(x.cuda())
+        outs["torch-folded"] = (p.cpu().numpy(), v.cpu().numpy().reshape(-1))
+    errs = {k: (float(np.abs(p - d["policy"]).max()), float(np.abs(v - d["value"]).max())) for k, (p, v) in outs.items()}
+    for k, (ep, ev) in errs.items():
+        assert ev <= 1e-5 and ep <= 1e-5, (k, errs)
+    # the net is not saturated: parity above is not hidden by tanh / softmax clamping
+    assert np.abs(d["value"]).max() < 0.95 and np.median(d["policy"].max(axis=1)) < 0.5
+
+
+def test_fused_outputs_do_not_depend_on_the_batch(gpu):
+    """A position's fused-evaluator outputs are bit-identical whether it is evaluated
+    alone, in a batch of 64, or at an odd offset inside a batch of 1,000 other positions
+    (per-board V scaling in the split-f16 tower): the evaluation cache's premise."""
+    import torch
+    from uttt_amd.model import calibrated_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    d = golden("netcal.npz")
+    r = golden("rules.npz")
+    mine = _rules_states(d["rules_index"][:64])
+    rng = np.random.RandomState(9)
+    others = _rules_states(rng.choice(np.nonzero(r["n_legal"] > 0)[0], 1000, replace=False))
+    net = calibrated_network(NETCAL, "cuda")
+    for conv in ("wino3h", "wino3"):
+        fe = FusedNetworkEvaluator(net, None, max_batch=1100, conv=conv)
+        p0, v0 = (t.clone() for t in fe.forward_states(mine))
+        big = np.concatenate([others[:37], mine, others[37:]])
+        p1, v1 = fe.forward_states(big)
+        assert torch.equal(p1[37:37 + 64], p0) and torch.equal(v1[37:37 + 64], v0), conv
+        for i in (0, 13, 63):
+            p2, v2 = fe.forward_states(mine[i:i + 1])
+            assert torch.equal(p2[0], p0[i]) and torch.equal(v2[0], v0[i]), (conv, i)
+
+
+def test_split_f16_conv_is_batch_independent(gpu):
+    """Conv-level form of the same property: 64 boards convolved alone and inside a batch
+    whose other boards are x1e3 / x1e-3 outliers give equal output bits (the V scale is per
+    board; a batch-wide scale would push these boards' low halves into f16 subnormals)."""
+    import torch
+    from uttt_amd.model import fold_bn, random_network
+    from uttt_amd.nnfast import conv3x3_wino3h, wino3h_weights
+    net = random_network(3)
+    w, b = fold_bn(net.residual_blocks[4].conv2, net.residual_blocks[4].bn2)
+    u, su = wino3h_weights(w)
+    u, b = u.cuda(), b.cuda()
+    g = torch.Generator().manual_seed(4)
+    x = torch.relu(torch.randn(64, 81, 128, generator=g)).cuda()
+    r = torch.randn(64, 81, 128, generator=g).cuda()
+    y0 = conv3x3_wino3h(x, u, su, b, r)
+    big = torch.relu(torch.randn(200, 81, 128, generator=g)).cuda()
+    big[5] *= 1e3
+    big[150] *= 1e-3
+    rbig = torch.randn(200, 81, 128, generator=g).cuda()
+    for off in (0, 3, 101, 136):
+        xb, rb = big.clone(), rbig.clone()
+        xb[off:off + 64], rb[off:off + 64] = x, r
+        xb[(off + 70) % 200] *= 1e3
+        yb = conv3x3_wino3h(xb, u, su, b, rb)
+        assert torch.equal(yb[off:off + 64], y0), off
 
 
 # ---------------------------------------------------------------- arena path --

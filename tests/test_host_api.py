@@ -115,36 +115,24 @@ def test_engine_requires_gpu_loudly():
         Engine(4, 50)
 
 
-def test_winograd_algebra_matches_direct_conv(engine_lib):
-    """Winograd F(2x2,3x3) as the kernel computes it (U from uttt_nn_wino_weights;
-    V = B^T d B on 4x4 windows of the zero-padded board; Y = A^T (U . V) A on
-    5x5 tiles, 10x10 outputs cropped to 9x9) equals the direct 3x3 conv."""
-    import ctypes
-    rng = np.random.RandomState(0)
-    w = rng.randn(128, 128, 3, 3).astype(np.float32)
-    u = np.zeros((16, 128, 128), np.float32)
-    fp = ctypes.POINTER(ctypes.c_float)
-    assert engine_lib.uttt_nn_wino_weights(w.ctypes.data_as(fp), u.ctypes.data_as(fp)) == 0
-    # stored order U[xi][ci/16][co][ci%2][(ci%16)/2] -> U[xi][ci][co]
-    u = u.reshape(16, 8, 128, 2, 8).transpose(0, 1, 4, 3, 2).reshape(16, 128, 128)
-    BT = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
-    AT = np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64)
-    x = rng.randn(9, 9, 128)
-    xp = np.zeros((12, 12, 128))
-    xp[1:10, 1:10] = x
-    y = np.zeros((10, 10, 128))
-    U = u.astype(np.float64).reshape(4, 4, 128, 128)
-    for ty in range(5):
-        for tx in range(5):
-            d = xp[2 * ty:2 * ty + 4, 2 * tx:2 * tx + 4]                  # (4,4,ci)
-            V = np.einsum("ui,ijc,vj->uvc", BT, d, BT)                    # (4,4,ci)
-            M = np.einsum("uvc,uvco->uvo", V, U)                          # (4,4,co)
-            y[2 * ty:2 * ty + 2, 2 * tx:2 * tx + 2] = np.einsum("au,uvo,bv->abo", AT, M, AT)
-    direct = np.zeros((9, 9, 128))
-    for ky in range(3):
-        for kx in range(3):
-            direct += np.einsum("rsc,oc->rso", xp[ky:ky + 9, kx:kx + 9], w[:, :, ky, kx].astype(np.float64))
-    assert np.abs(y[:9, :9] - direct).max() < 1e-4 * np.abs(direct).max()
+def test_calibrated_network_reproduces_reference_fixture():
+    """tests/golden/netcal.npz pins the non-saturated network the GPU parity tests use: the
+    seed-0 DualNetwork + the fixture's BatchNorm statistics (uttt_amd.model.calibrated_network)
+    has the reference's parameters (per-tensor sums) and reproduces the reference's CPU fp32
+    outputs; and the net is genuinely unsaturated."""
+    import torch
+    from uttt_amd.model import calibrated_network
+    d = golden("netcal.npz")
+    net = calibrated_network(os.path.join(GOLDEN, "netcal.npz"))
+    sd = net.state_dict()
+    sums = np.asarray([t.double().sum().item() for t in sd.values()])
+    floats = np.asarray([t.is_floating_point() for t in sd.values()])  # not num_batches_tracked
+    assert np.allclose(sums[floats], d["param_sums"][floats], rtol=1e-9, atol=1e-9)
+    with torch.no_grad():
+        p, v = net(torch.from_numpy(d["x"].astype(np.float32)))
+    assert np.abs(p.numpy() - d["policy"]).max() <= 1e-6
+    assert np.abs(v.numpy().reshape(-1) - d["value"]).max() <= 1e-6
+    assert np.abs(d["value"]).max() < 0.95 and np.median(d["policy"].max(axis=1)) < 0.5
 
 
 def test_winograd3_algebra_matches_direct_conv(engine_lib):

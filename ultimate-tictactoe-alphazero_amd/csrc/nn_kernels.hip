@@ -4,7 +4,6 @@
 //   k_stem      leaf bitboards -> relu(conv3x3(3->128) + b), written NHWC. The input
 //               planes (own, opponent, legal; uttt_game.cpp:244-280) are 0/1, so the
 //               conv is a masked sum of 27 weight rows; no NCHW tensor is built.
-//   k_epilogue  relu(conv + b [+ residual]) in one pass (MIOpen computes the bare conv).
 //   k_heads     1x1 convs (128->2, 128->1) + ReLU, policy FC 162->81 + softmax,
 //               value FC 81->256 + ReLU + FC 256->1 + tanh: four positions per workgroup.
 #include <hip/hip_runtime.h>
@@ -47,7 +46,7 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
     const int t = threadIdx.x;
     for (int i = t; i < 27 * (C / 4); i += 256) s_w[i] = reinterpret_cast<const float4 *>(w)[i];
     for (int i = t; i < nb * 81; i += 256) {
-        const uttt_state_t s = leaf[tree_of[s0 + i / 81]];
+        const uttt_state_t s = leaf[tree_of ? tree_of[s0 + i / 81] : s0 + i / 81];
         uint32_t lm[3];
         legal_mask(s, lm);
         const int pos = i % 81, R = pos / 9, Cc = pos % 9;
@@ -84,32 +83,6 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
         acc.z = fmaxf(acc.z, 0.0f);
         acc.w = fmaxf(acc.w, 0.0f);
         o[i] = acc;
-    }
-}
-
-// y = relu(x + bias[c] (+ r)), NHWC rows of C channels, float4 per thread, grid-stride.
-__global__ __launch_bounds__(256) void k_epilogue(const float *__restrict__ x, const float *__restrict__ bias,
-                                                  const float *__restrict__ r, float *__restrict__ y, int64_t n4) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        float4 v = reinterpret_cast<const float4 *>(x)[i];
-        const float4 bb = reinterpret_cast<const float4 *>(bias)[i % (C / 4)];
-        v.x += bb.x;
-        v.y += bb.y;
-        v.z += bb.z;
-        v.w += bb.w;
-        if (r) {
-            const float4 rv = reinterpret_cast<const float4 *>(r)[i];
-            v.x += rv.x;
-            v.y += rv.y;
-            v.z += rv.z;
-            v.w += rv.w;
-        }
-        v.x = fmaxf(v.x, 0.0f);
-        v.y = fmaxf(v.y, 0.0f);
-        v.z = fmaxf(v.z, 0.0f);
-        v.w = fmaxf(v.w, 0.0f);
-        reinterpret_cast<float4 *>(y)[i] = v;
     }
 }
 
@@ -254,19 +227,18 @@ int uttt_nn_stem(uttt_engine_t *e, const float *w, const float *b, float *out) {
     return UTTT_OK;
 }
 
-int uttt_nn_epilogue(const float *x, const float *bias, const float *residual, float *y, int64_t rows,
-                     int32_t channels, void *stream) {
-    if (!x || !bias || !y || rows < 0 || channels != nn::C) {
-        set_error("uttt_nn_epilogue: bad arguments (channels must be %d)", nn::C);
+int uttt_nn_stem_states(const uttt_state_t *states, int32_t n, const float *w, const float *b, float *out,
+                        void *stream) {
+    if (!states || !w || !b || !out || n < 0) {
+        set_error("uttt_nn_stem_states: bad arguments");
         return UTTT_ERR_ARG;
     }
-    const int64_t n4 = rows * channels / 4;
-    if (n4 == 0) return UTTT_OK;
-    int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 256 * 16);
-    hipLaunchKernelGGL(nn::k_epilogue, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, bias, residual, y, n4);
+    if (n == 0) return UTTT_OK;
+    hipLaunchKernelGGL(nn::k_stem, dim3((n + nn::SB - 1) / nn::SB), dim3(256), 0, (hipStream_t)stream, states, nullptr, n,
+                       w, b, out);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
-        set_error("k_epilogue launch: %s", hipGetErrorString(r));
+        set_error("k_stem launch: %s", hipGetErrorString(r));
         return UTTT_ERR_HIP;
     }
     return UTTT_OK;

@@ -344,9 +344,9 @@ __global__ __launch_bounds__(NT) void k_wino3_conv(const float *__restrict__ x, 
     float4 xr[XPT];
     const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(u), 0, NP * C * C * 4, 0x00020000);
     const int voff = (co * 4 + (lane >> 4)) * 16;
-    // Chunk order rotated per workgroup: concurrent workgroups read different U
-    // blocks instead of all hammering the same 8 KB of L2 at once.
-    const int c_rot = blockIdx.x % NCH;
+    // Every workgroup takes the chunks in the same order: the f32 accumulation order of a
+    // board's results must not depend on which workgroup (= where in the batch) it lands.
+    const int c_rot = 0;
     auto chunk_of = [&](int g) { return (g % NCH + c_rot) % NCH; };
     floatx4 b0v = load_b(ur, 0, c_rot, voff), b1v = load_b(ur, 1, c_rot, voff), b2v = load_b(ur, 2, c_rot, voff);
     const float bb = bias[co];

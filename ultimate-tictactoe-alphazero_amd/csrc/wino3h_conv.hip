@@ -13,13 +13,17 @@
 // i.e. three v_mfma_f32_16x16x32_f16 per 32-channel k-step where the f32 form
 // needs eight v_mfma_f32_16x16x4_f32 per 16 channels: 16.5 against 32 cycles
 // per instruction on gfx950 (tools/diag/mfma_rate.hip), 5.2x fewer MFMA cycles
-// per MAC. The dropped V_lo U_lo term is ~2^-22 relative. To keep both halves
-// in f16's range, V is scaled by a power of two sv chosen from the input's
-// maximum (|V| <= 36 max|x|, so 36 max|x| sv <= 2^15) and U by su from its own
-// maximum (host); the epilogue multiplies by 1/(sv su) (exact). The input
-// maximum comes from the producer: every conv's epilogue (and the caller for
-// the stem output) atomically maxes its output into a u32 slot, so no extra
-// pass is needed. Error against an f64 direct conv: DESIGN.md §5.
+// per MAC. The dropped V_lo U_lo term is ~2^-22 relative (both splits round to nearest). To keep both halves
+// in f16's range, V is scaled by a power of two sv chosen PER BOARD from that
+// board's input maximum (|V| <= 36 max|x|, so 36 max|x| sv <= 2^15) and U by su
+// from its own maximum (host); the epilogue multiplies each tile's results by
+// 1/(sv su) of its board (exact). A board's outputs therefore depend on that
+// board's inputs only, never on the other boards of the batch (the evaluation
+// cache replays outputs across forwards, engine.hip). The per-board maxima come
+// from the producer: every conv's epilogue atomically maxes its outputs into a
+// u32 slot per board (the stem output uses one weight-derived bound for all
+// boards), so no extra pass is needed. Error against an f64 direct conv:
+// DESIGN.md §5.
 //
 // Workgroup = 8 waves, one set = 32 tile slots x 128 output channels; wave w owns
 // channels 16w..16w+15. The 63 tiles of 7 consecutive boards are two sets (tiles
@@ -248,14 +252,24 @@ __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restric
     }
 }
 
-// registers -> sX[padded position][32 channels], scaled by sv (a power of two: exact)
-__device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&xr)[XPT], float sv, int tid) {
+// Per-board V scales of the SB staged boards of a set (powers of two, uniform over the workgroup)
+struct SetScale {
+    float s[SB];
+    __device__ __forceinline__ float of(int kb) const {
+        // a select chain, not a dynamically indexed array (that would live in scratch)
+        return kb == 0 ? s[0] : (kb == 1 ? s[1] : (kb == 2 ? s[2] : s[3]));
+    }
+};
+
+// registers -> sX[padded position][32 channels], scaled by its board's sv (a power of two: exact)
+__device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&xr)[XPT], const SetScale &sc, int tid) {
 #pragma unroll
     for (int k = 0; k < XPT; ++k) {
         const int i = tid + k * NT;
         if (i < XF4) {
             const int q = i % (KC / 4), bp = i / (KC / 4);
             const int kb = bp / 81, pos = bp - 81 * kb, sp = spos(kb, pos / 9, pos % 9);
+            const float sv = sc.of(kb);
             float4 v = xr[k];
             v.x *= sv;
             v.y *= sv;
@@ -281,12 +295,13 @@ __device__ __forceinline__ void bt5(const floatx2 (&d)[5], floatx2 (&t)[5]) {
     t[4] = __builtin_elementwise_fma(mtwo, t3, h);
 }
 
-// (v0, v1) -> packed f16 hi (round toward zero) and f16 lo = the remainder
+// (v0, v1) -> packed f16 hi (round to nearest: |v - hi| <= 2^-11 |v|, exact in f32) and
+// f16 lo = the remainder rounded to nearest (v_cvt_pk_f16_f32, one instruction each)
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split(floatx2 v, uint32_t &hi, uint32_t &lo) {
-    const auto h = __builtin_amdgcn_cvt_pkrtz(v.x, v.y);
-    const floatx2 hf = {(float)h[0], (float)h[1]};
-    const floatx2 r = v - hf;
-    const auto l = __builtin_amdgcn_cvt_pkrtz(r.x, r.y);
+    const halfx2 h = __builtin_convertvector(v, halfx2);
+    const floatx2 r = v - __builtin_convertvector(h, floatx2);
+    const halfx2 l = __builtin_convertvector(r, halfx2);
     hi = __builtin_bit_cast(uint32_t, h);
     lo = __builtin_bit_cast(uint32_t, l);
 }
@@ -367,6 +382,19 @@ __device__ __forceinline__ float pow2_scale(float amax) {
     return ldexpf(1.0f, e);
 }
 
+// V scales of the staged boards b0 .. b0+SB-1 (boards past the end: 1). x_amax holds one
+// max per board (per_board) or one bound for every board.
+__device__ __forceinline__ SetScale set_scale(const uint32_t *__restrict__ x_amax, int per_board, int b0, int n_boards) {
+    SetScale sc;
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+        const int b = b0 + k;
+        const uint32_t bits = per_board ? (b < n_boards ? x_amax[b] : 0u) : x_amax[0];
+        sc.s[k] = pow2_scale(__builtin_bit_cast(float, bits));
+    }
+    return sc;
+}
+
 // MODE+4 phase stamps (core clocks, s_memtime) of workgroups 0..63, waves 0 and 4, first 8
 // chunks: per chunk [after load_x issue, after transform, after barrier+store_x, after GEMMs,
 // after epilogue, after closing barrier] relative to the chunk's start.
@@ -381,13 +409,16 @@ template <bool RES, int MODE = 0, int PF = 3>
 __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
                                                     float u_scale, const float *__restrict__ bias,
                                                     const float *__restrict__ res, float *__restrict__ y,
-                                                    const uint32_t *__restrict__ x_amax, uint32_t *__restrict__ y_amax,
-                                                    int n_boards) {
+                                                    const uint32_t *__restrict__ x_amax, int x_amax_per_board,
+                                                    uint32_t *__restrict__ y_amax, uint32_t *__restrict__ amax_clear,
+                                                    int clear_count, int n_boards) {
     // sX [padded position][channel] (border = 0) then sV
     __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
     float *const sX = reinterpret_cast<float *>(smem);
     char *const sV = smem + XP * KC * 4;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // zero the per-board max row a later conv of this forward accumulates into
+    for (int i = (int)blockIdx.x * NT + tid; i < clear_count; i += (int)gridDim.x * NT) amax_clear[i] = 0u;
     const int nsets = n_sets(n_boards);
     if ((int)blockIdx.x >= nsets) return;
     const int my_sets = (nsets - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
@@ -395,8 +426,6 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     auto set_of = [&](int g) { return (int)blockIdx.x + (g / NCH) * (int)gridDim.x; };
     auto set_b0 = [&](int g) { const int st = set_of(g); return GB * (st >> 1) + 3 * (st & 1); };  // first staged board
     const int co = wv * 16 + (lane & 15);
-    const float sv_scale = pow2_scale(__builtin_bit_cast(float, *x_amax));
-    const float inv = 1.0f / (sv_scale * u_scale);  // both powers of two: exact
     const int co4 = wv * 16 + 4 * (lane >> 4);  // the 4 output channels of this lane's MFMA results
     const floatx4 bb4 = *reinterpret_cast<const floatx4 *>(bias + co4);
 
@@ -412,7 +441,9 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(ub), 0, NP * C * C * 4, 0x00020000);
     const int kq = lane >> 4;
     const int voff = (co * 4 + kq) * 16;
-    const int c_rot = blockIdx.x % NCH;
+    // Every workgroup takes the chunks in the same order: the f32 accumulation order of a
+    // board's results must not depend on which workgroup (= where in the batch) it lands.
+    const int c_rot = 0;
     auto chunk_of = [&](int g) { return (g % NCH + c_rot) % NCH; };
     const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (4 * kq)) * 16);
 
@@ -423,7 +454,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
 #pragma unroll
     for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, c_rot, voff);
     load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
-    store_x(sX, xr, sv_scale, tid);
+    store_x(sX, xr, set_scale(x_amax, x_amax_per_board, set_b0(0), n_boards), tid);
     __syncthreads();
     const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
     auto mark = [&](int g, int k, unsigned long long t0) {
@@ -436,11 +467,12 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         // the next chunk's inputs load during this chunk's transform (registers are
         // free then; the point loop needs nearly all of them)
         if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+        const SetScale sc_next = set_scale(x_amax, x_amax_per_board, set_b0(g + 1), n_boards);
         mark(g, 0, t0);
         if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid), set_of(g) & 1);
         mark(g, 1, t0);
         lds_barrier();
-        if (g + 1 < G) store_x(sX, xr, sv_scale, fresh(tid));
+        if (g + 1 < G) store_x(sX, xr, sc_next, fresh(tid));
         mark(g, 2, t0);
         if constexpr ((MODE & 3) != 2) {
             AFrag a0 = load_a(sv_lane, 0);
@@ -453,22 +485,28 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             // of tile slot 16rt + (lane & 15)
             const int st = set_of(g), grp = st >> 1, h = st & 1;
             const int el = fresh(lane);
+            const SetScale sc = set_scale(x_amax, x_amax_per_board, set_b0(g), n_boards);
             // Straight from registers: the MFMA output puts 4 consecutive channels of one tile
             // in a lane (U is the A operand), so every output position is one 16-byte store
             // (+ one 16-byte residual load, issued before Y is formed); no LDS round trip and
             // no barrier.
             size_t off[2];
             bool live[2];
+            int board_of[2];
+            float inv[2];
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt) {
                 const int gt = 32 * h + 16 * rt + (el & 15), gb = gt / 9, tt = gt - 9 * gb;
                 const int board = GB * grp + gb;
                 live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
                 off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4;
+                board_of[rt] = board;
+                // this tile's board's V scale times su: both powers of two, so 1/x is exact
+                inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
             }
-            float vmax = 0.0f;
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt) {
+                float vmax = 0.0f;
                 // tile block rt: residual loads first (in flight while Y is formed)
                 floatx4 rv[9];
                 if constexpr (RES) {
@@ -502,12 +540,11 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                     S[i].p[2 * rt] = floatx2{0.0f, 0.0f};
                     S[i].p[2 * rt + 1] = floatx2{0.0f, 0.0f};
                 }
-                if (!live[rt]) continue;
 #pragma unroll
-                for (int ab = 0; ab < 9; ++ab) {
+                for (int ab = 0; ab < 9 && live[rt]; ++ab) {
                     floatx4 v;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv, bb4[r]);
+                    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv[rt], bb4[r]);
                     if constexpr (RES) v += rv[ab];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.0f);
@@ -521,11 +558,14 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                     }
                     vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
                 }
-            }
-            if (y_amax) {
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
-                if (lane == 0) atomicMax(y_amax, __builtin_bit_cast(uint32_t, vmax));  // v >= 0: bit order = value order
+                if (y_amax) {
+                    // the 4 lanes of a tile (lane bits 4-5: channel quads) -> one max per tile,
+                    // then one atomic per (tile, wave) into its board's slot
+                    vmax = fmaxf(vmax, __shfl_xor(vmax, 16));
+                    vmax = fmaxf(vmax, __shfl_xor(vmax, 32));
+                    if (el < 16 && live[rt])  // v >= 0: u32 bit order = value order
+                        atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
+                }
             }
         }
         mark(g, 4, t0);
@@ -620,20 +660,24 @@ int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale) {
 }
 
 int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *residual,
-                           float *y, const uint32_t *x_amax, uint32_t *y_amax, int32_t n_boards, void *stream) {
+                           float *y, const uint32_t *x_amax, int32_t x_amax_per_board, uint32_t *y_amax,
+                           uint32_t *amax_clear, int32_t clear_count, int32_t n_boards, void *stream) {
     if (!x || !u || !bias || !y || !x_amax || n_boards < 0 || x == y || (residual && residual == y) ||
-        !(u_scale > 0.0f)) {
-        set_error("uttt_nn_conv3x3_wino3h: bad arguments (x_amax required; output must not alias input or residual)");
+        !(u_scale > 0.0f) || clear_count < 0 || (clear_count > 0 && !amax_clear) ||
+        (amax_clear && (amax_clear == y_amax || amax_clear == x_amax))) {
+        set_error("uttt_nn_conv3x3_wino3h: bad arguments (x_amax required; output must not alias input or residual; "
+                  "the cleared max row must differ from x_amax and y_amax)");
         return UTTT_ERR_ARG;
     }
-    if (n_boards == 0) return UTTT_OK;
-    const dim3 grid(wino3h::grid_size(n_boards));
+    if (n_boards == 0 && clear_count == 0) return UTTT_OK;
+    const dim3 grid(wino3h::grid_size(n_boards > 0 ? n_boards : 1));
+    const int pb = x_amax_per_board ? 1 : 0;
     if (residual)
         hipLaunchKernelGGL(wino3h::k_wino3h_conv<true>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
-                           bias, residual, y, x_amax, y_amax, n_boards);
+                           bias, residual, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards);
     else
         hipLaunchKernelGGL(wino3h::k_wino3h_conv<false>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
-                           bias, nullptr, y, x_amax, y_amax, n_boards);
+                           bias, nullptr, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_wino3h_conv launch: %s", hipGetErrorString(r));
@@ -666,24 +710,24 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
     hipStream_t st = (hipStream_t)stream;
     using namespace wino3h;
     switch (mode) {
-        case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 16: hipLaunchKernelGGL((k_wino3h_conv<false, 16>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 32: hipLaunchKernelGGL((k_wino3h_conv<false, 32>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 48: hipLaunchKernelGGL((k_wino3h_conv<false, 48>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 68: hipLaunchKernelGGL((k_wino3h_conv<false, 68>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 116: hipLaunchKernelGGL((k_wino3h_conv<false, 116>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 20: hipLaunchKernelGGL((k_wino3h_conv<false, 20>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards);
+        case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 16: hipLaunchKernelGGL((k_wino3h_conv<false, 16>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 32: hipLaunchKernelGGL((k_wino3h_conv<false, 32>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 48: hipLaunchKernelGGL((k_wino3h_conv<false, 48>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 68: hipLaunchKernelGGL((k_wino3h_conv<false, 68>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 116: hipLaunchKernelGGL((k_wino3h_conv<false, 116>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 20: hipLaunchKernelGGL((k_wino3h_conv<false, 20>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
     }
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }
@@ -701,11 +745,11 @@ int uttt_diag_wino3h_pf(const float *x, const uint16_t *u, float u_scale, const 
     hipStream_t st = (hipStream_t)stream;
     using namespace wino3h;
     switch (pf) {
-        case 3: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 6: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 6>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards); break;
-        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, nullptr, n_boards);
+        case 3: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 6: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 6>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
     }
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }

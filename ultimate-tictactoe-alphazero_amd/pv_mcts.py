@@ -69,7 +69,7 @@ def _search(evaluate_count):
 
 def pv_mcts_scores(model, state, temperature):
     s = _search(PV_EVALUATE_COUNT)
-    (v,) = s.visits([state], model_evaluator(model, 1), PV_EVALUATE_COUNT, MCTS_BATCH_SIZE)
+    (v,) = s.visits([state], model_evaluator(model, 1, s.engine), PV_EVALUATE_COUNT, MCTS_BATCH_SIZE)
     return scores_from_visits(v, temperature)
 
 

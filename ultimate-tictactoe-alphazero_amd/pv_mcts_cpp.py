@@ -31,10 +31,31 @@ def _model_device(model):
     return device
 
 
-def make_inference_func(model):
+def make_inference_func(model, evaluator=None):
     """The flush callback: list of uttt_cpp.State -> [(policy (81,) f32, value float)].
-    Inputs are the states' HWC tensors stacked and moved to NCHW, as the
-    reference builds them (pv_mcts_cpp.py:47-60)."""
+
+    For a DualNetwork (the reference's or this package's) the states go straight to the fused
+    HIP evaluator (stem from the packed bitboards, Winograd tower, heads; within 1e-5 of the
+    model's own forward, tests/test_engine_gpu.py); for any other model, or with
+    evaluator="torch" / UTTT_EVALUATOR=torch, the states' HWC tensors are stacked and moved to
+    NCHW as the reference builds them (pv_mcts_cpp.py:47-60) and the model is called."""
+    from uttt_amd.nnfast import FusedNetworkEvaluator, evaluator_kind
+    if torch.cuda.is_available() and evaluator_kind(model, evaluator) == "fused":
+        from uttt_amd import as_states
+        dev = _model_device(model)
+        dev = dev if dev.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+        box = {}
+
+        def fused_inference(states_list):
+            n = len(states_list)
+            fe = box.get("fe")
+            if fe is None or fe.max_batch < n:
+                fe = box["fe"] = FusedNetworkEvaluator(model, None, max_batch=max(64, n), device=dev)
+            p, v = fe.forward_states(as_states(states_list))
+            p, v = p.cpu().numpy(), v.cpu().numpy()
+            return [(p[i], float(v[i])) for i in range(n)]
+
+        return fused_inference
     dev = _model_device(model)
 
     def inference_func(states_list):
@@ -53,8 +74,8 @@ def pv_mcts_scores_cpp(model, state, temperature, evaluate_count=50, batch_size=
     if not CPP_AVAILABLE:
         raise RuntimeError("C++ module is not available. Please build uttt_cpp first.")
     model.eval()
-    scores = uttt_cpp.pv_mcts_scores(model=make_inference_func(model), state=state, temperature=temperature,
-                                     evaluate_count=evaluate_count, batch_size=batch_size)
+    scores = uttt_cpp.pv_mcts_scores(model=make_inference_func(model), state=_to_engine_state(state),
+                                     temperature=temperature, evaluate_count=evaluate_count, batch_size=batch_size)
     return np.array(scores)
 
 

@@ -81,9 +81,14 @@ class ModelEvaluator:
         return p.to(x.device).float(), v.to(x.device).float().reshape(n, -1)
 
 
-def model_evaluator(model, max_batch=None):
-    """Engine evaluator for a model: NetworkEvaluator when it lives on the GPU (no copies),
+def model_evaluator(model, max_batch=None, engine=None, kind=None):
+    """Engine evaluator for a model: the fused HIP evaluator for a DualNetwork (given the engine;
+    nnfast.evaluator_kind), else NetworkEvaluator when the model lives on the GPU (no copies),
     ModelEvaluator otherwise."""
+    if engine is not None:
+        from .nnfast import FusedNetworkEvaluator, evaluator_kind
+        if evaluator_kind(model, kind) == "fused":
+            return FusedNetworkEvaluator(model, engine)
     dev = next((p.device for p in model.parameters()), None)
     if dev is not None and dev.type == "cuda" and max_batch:
         model.eval()
@@ -100,7 +105,8 @@ def evaluate_network(model0, model1, game_count=50, temperature=1.0, seed_base=0
     import uttt_cpp
     searches = [PvMcts(game_count, evaluate_count, device) for _ in range(2)]
     if make_evaluator is None:
-        evaluators = (model_evaluator(model0, game_count), model_evaluator(model1, game_count))
+        evaluators = (model_evaluator(model0, game_count, searches[0].engine),
+                      model_evaluator(model1, game_count, searches[1].engine))
     else:
         evaluators = (make_evaluator(model0, searches[0].engine), make_evaluator(model1, searches[1].engine))
     states = [uttt_cpp.State() for _ in range(game_count)]
@@ -146,7 +152,7 @@ def self_play_py(model, game_count, seed_base=0, temperature=1.0, evaluate_count
     illegal actions), value (first_player_value at ply 0, then alternating)]."""
     import uttt_cpp
     search = PvMcts(game_count, evaluate_count, device)
-    ev = make_evaluator(model, search.engine) if make_evaluator else model_evaluator(model, game_count)
+    ev = make_evaluator(model, search.engine) if make_evaluator else model_evaluator(model, game_count, search.engine)
     states = [uttt_cpp.State() for _ in range(game_count)]
     rngs = [np.random.RandomState(seed_base + g) for g in range(game_count)]
     hist = [[] for _ in range(game_count)]

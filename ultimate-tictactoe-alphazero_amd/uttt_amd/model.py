@@ -146,3 +146,28 @@ def policy_logits(net, x):
 def random_network(seed=0, device="cpu"):
     torch.manual_seed(seed)
     return DualNetwork().to(device).eval()
+
+
+def calibrated_network(npz_path, device="cpu"):
+    """The non-saturated test/bench network of tests/golden/netcal.npz: the seed-0 DualNetwork
+    (as the reference initialises it) with the fixture's calibrated BatchNorm running statistics
+    and value_fc2.weight scaled by the fixture's power of two (tests/golden/make_golden.py
+    gen_netcal). Its outputs are O(1) values and spread policies, so network parity is not
+    hidden behind tanh/softmax saturation."""
+    import numpy as np
+    with np.load(npz_path) as z:
+        names = [str(s) for s in z["bn_names"]]
+        mean, var, sizes = z["bn_mean"], z["bn_var"], z["bn_sizes"]
+        scale = float(z["vfc2_scale"])
+    torch.manual_seed(0)
+    net = DualNetwork()
+    mods = dict(net.named_modules())
+    o = 0
+    with torch.no_grad():
+        for name, k in zip(names, sizes.tolist()):
+            bn = mods[name]
+            bn.running_mean.copy_(torch.from_numpy(mean[o:o + k]))
+            bn.running_var.copy_(torch.from_numpy(var[o:o + k]))
+            o += k
+        net.value_fc2.weight.mul_(scale)
+    return net.to(device).eval()

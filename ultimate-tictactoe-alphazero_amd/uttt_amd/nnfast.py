@@ -1,27 +1,28 @@
 """FusedNetworkEvaluator: the DualNetwork leaf evaluator as gfx950 kernels
-(csrc/nn_kernels.hip, csrc/wino_conv.hip, include/uttt_nn.h):
+(csrc/nn_kernels.hip, csrc/wino3h_conv.hip, csrc/wino3_conv.hip, include/uttt_nn.h):
 
-  leaves --k_stem--> act (n,9,9,128 NHWC, relu(conv_input+bn) applied)
-  16 x [ conv3x3 + b1 + ReLU            (conv="wino3h": Winograd F(3x3,3x3), split-f16 MFMA,
-         conv3x3 + b2 + residual + ReLU ]  conv="wino3": the same on f32 MFMA,
-                                           conv="wino": Winograd F(2x2,3x3), f32 MFMA,
-                                           conv="miopen": MIOpen NHWC conv + k_epilogue)
+  leaves --k_stem--> act (n,81,128 NHWC, relu(conv_input+bn) applied, straight from bitboards)
+  16 x [ conv3x3 + b1 + ReLU            (conv="wino3h", default: Winograd F(3x3,3x3), split-f16
+         conv3x3 + b2 + residual + ReLU ]  MFMA, f32 accumulation; conv="wino3": the same on the
+                                           f32 MFMA)
   --k_heads--> policy (n,81) softmax, value (n,)
 
-Replaces, per forward, the engine's NCHW encode, MIOpen's stem conv (naive /
-ck grouped kernels for 3 input channels), every separate bias / ReLU / add
-pass, and the head convs + FCs. BatchNorm is folded (eval mode), so the
-function is the reference's dual_network.py:89-121 up to fp32 rounding order.
+BatchNorm is folded (eval mode), so the function is the reference's
+dual_network.py:89-121 up to fp32 rounding order (tests/test_engine_gpu.py
+bounds value and post-softmax policy at 1e-5 against the reference's own CPU
+fp32 outputs on a non-saturated network). Every kernel computes a board from
+that board's inputs alone (the split-f16 V scale is per board), so a position's
+outputs are bit-identical whatever batch it is evaluated in - the premise of
+the engine's evaluation cache and of lane/GPU-count invariance.
 """
 import ctypes
+import weakref
 
 import torch
-import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check
 from .model import fold_bn
-from .selfplay import _bucket
 
 HEAD = {}
 
@@ -58,134 +59,141 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-class FusedNetworkEvaluator:
-    needs_input = False
-    AMAX_RING = 64
+_WEIGHTS = weakref.WeakKeyDictionary()  # model -> {(device, conv): (fingerprint, prepared weights)}
 
-    def __init__(self, net, engine, max_batch=None, conv="wino3h"):
+
+def _fingerprint(net):
+    """Changes whenever a parameter or buffer is replaced or modified in place (optimizer
+    steps, load_state_dict): tensors' version counters are shared with their detached views."""
+    return tuple((t.data_ptr(), t._version) for t in net.state_dict().values())
+
+
+@torch.no_grad()
+def _prepared_weights(net, dev, conv):
+    """BN-folded, kernel-ordered weights of a DualNetwork on `dev` (cached per model, device and
+    kernel; rebuilt when the model's weights change)."""
+    fp = _fingerprint(net)
+    per = _WEIGHTS.setdefault(net, {})
+    key = (str(dev), conv)
+    hit = per.get(key)
+    if hit is not None and hit[0] == fp:
+        return hit[1]
+    sw, sb = fold_bn(net.conv_input, net.bn_input)            # (128,3,3,3)
+    out = {"stem_w": sw.permute(1, 2, 3, 0).reshape(27, 128).contiguous().to(dev),
+           "stem_b": sb.contiguous().to(dev), "heads": pack_heads(net, dev), "wino": []}
+    for b in net.residual_blocks:
+        pair = []
+        for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
+            w, bb = fold_bn(cv, bn)
+            if conv == "wino3h":
+                u, su = wino3h_weights(w)
+                pair.append((u.to(dev), su, bb.to(dev)))
+            else:
+                pair.append((wino3_weights(w).to(dev), None, bb.to(dev)))
+        out["wino"].append(tuple(pair))
+    # the stem's output bound for every board: relu(b + sum of the positive weight rows), inputs 0/1
+    out["stem_bound"] = float(torch.relu(out["stem_b"].double().cpu() +
+                                         out["stem_w"].double().cpu().clamp_min(0).sum(0)).max())
+    per[key] = (fp, out)
+    return out
+
+
+class FusedNetworkEvaluator:
+    """Leaf evaluator over an engine's pending leaves (needs_input = False: the stem reads
+    the leaves' bitboards, the engine never builds the NCHW tensor)."""
+    needs_input = False
+    NROW = 4  # per-board max rows, rotated over the 32 convs (see __init__, _tower_heads)
+
+    def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None):
         net = net.eval()
-        assert conv in ("wino3h", "wino3", "wino", "miopen")
+        if conv not in ("wino3h", "wino3"):
+            raise ValueError("conv must be 'wino3h' or 'wino3'")
         self.conv = conv
         self.engine = engine
         self.lib = _lib.load()
-        dev = torch.device("cuda", engine.device)
-        self.max_batch = max_batch or engine.max_trees
-        with torch.no_grad():
-            sw, sb = fold_bn(net.conv_input, net.bn_input)            # (128,3,3,3)
-            self.stem_w = sw.permute(1, 2, 3, 0).reshape(27, 128).contiguous().to(dev)
-            self.stem_b = sb.contiguous().to(dev)
-            cl = torch.channels_last
-            self.blocks = []
-            for b in net.residual_blocks:
-                w1, b1 = fold_bn(b.conv1, b.bn1)
-                w2, b2 = fold_bn(b.conv2, b.bn2)
-                self.blocks.append((w1.to(dev).contiguous(memory_format=cl), b1.to(dev),
-                                    w2.to(dev).contiguous(memory_format=cl), b2.to(dev)))
-            self.heads = pack_heads(net, dev)
-            if conv == "wino3h":
-                self.wino = []
-                for b in net.residual_blocks:
-                    pair = []
-                    for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
-                        w, bb = fold_bn(cv, bn)
-                        u, su = wino3h_weights(w)
-                        pair.append((u.to(dev), su, bb.to(dev)))
-                    self.wino.append(tuple(pair))
-                self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
-                # per-forward maxima: slot 0 bounds the stem output (inputs are 0/1 planes:
-                # relu(b + sum of the positive weight rows)), slot i+1 = max of conv i's output.
-                # Forwards take fresh slots from a ring that is zeroed once per AMAX_RING
-                # forwards: a per-forward fill kernel would wait for a free CU behind the
-                # other lanes' persistent convolutions.
-                nconv = 2 * len(self.wino)
-                self.amax_stride = nconv + 1
-                self.amax = torch.zeros(self.AMAX_RING * self.amax_stride, dtype=torch.float32, device=dev)
-                self.stem_bound = float(torch.relu(self.stem_b.double().cpu() +
-                                                   self.stem_w.double().cpu().clamp_min(0).sum(0)).max())
-                self.amax[::self.amax_stride] = self.stem_bound
-                self.amax = self.amax.view(torch.int32)
-                self.amax_pos = 0
-            elif conv in ("wino", "wino3"):
-                wfn = wino3_weights if conv == "wino3" else wino_weights
-                self.conv_fn = self.lib.uttt_nn_conv3x3_wino3 if conv == "wino3" else self.lib.uttt_nn_conv3x3_wino
-                self.wino = []
-                for b in net.residual_blocks:
-                    pair = []
-                    for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
-                        w, bb = fold_bn(cv, bn)
-                        pair += [wfn(w).to(dev), bb.to(dev)]
-                    self.wino.append(tuple(pair))
-                self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
-        self.act = torch.zeros((self.max_batch, 9, 9, 128), dtype=torch.float32, device=dev)
+        if engine is not None:
+            dev = torch.device("cuda", engine.device)
+            self.max_batch = max_batch or engine.max_trees
+        else:
+            dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            if max_batch is None:
+                raise ValueError("max_batch is required without an engine")
+            self.max_batch = max_batch
+        self.device = dev
+        self.nconv = 2 * len(net.residual_blocks)
+        if self.nconv % self.NROW:
+            raise ValueError("the max-row rotation needs a multiple of 4 convolutions")
+        w = _prepared_weights(net, dev, conv)
+        self.stem_w, self.stem_b, self.heads, self.wino = w["stem_w"], w["stem_b"], w["heads"], w["wino"]
+        self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
+        if conv == "wino3h":
+            # The stem's output is bounded for every board by relu(b + sum of the positive weight
+            # rows) (its inputs are 0/1 planes): one scale for all boards. Conv i then reads the
+            # per-board maxima of its input from row (i-1) % 4, atomically maxes its own output
+            # into row i % 4 and zeroes row (i+1) % 4 for conv i+1; 32 convs per forward keep
+            # the rotation aligned across forwards, so no fill kernel is ever needed.
+            self.stem_bound = w["stem_bound"]
+            self.stem_amax = torch.tensor([self.stem_bound], dtype=torch.float32, device=dev).view(torch.int32)
+            self.bamax = torch.zeros((self.NROW, self.max_batch), dtype=torch.int32, device=dev)
         self.policy = torch.zeros((self.max_batch, 81), dtype=torch.float32, device=dev)
         self.value = torch.zeros((self.max_batch,), dtype=torch.float32, device=dev)
+        self.states = None
 
-    def _epilogue(self, x, bias, res, out, stream):
-        check(self.lib.uttt_nn_epilogue(_p(x), _p(bias), _p(res) if res is not None else None, _p(out),
-                                        x.numel() // 128, 128, ctypes.c_void_p(stream)))
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     @torch.no_grad()
     def forward(self, n, softmax=True):
         """Evaluate the engine's n pending leaves; returns (policy or logits (n,81), value (n,))."""
-        if self.conv != "miopen":
-            return self._forward_wino(n, softmax)
-        stream = torch.cuda.current_stream(self.engine.device).cuda_stream
-        nb = _bucket(n, self.max_batch)
-        check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(self.act)))
-        a = self.act[:nb].permute(0, 3, 1, 2)  # NCHW view, channels-last strides
-        for w1, b1, w2, b2 in self.blocks:
-            y = F.conv2d(a, w1, None, padding=1)
-            assert y.is_contiguous(memory_format=torch.channels_last)
-            self._epilogue(y, b1, None, y, stream)
-            z = F.conv2d(y, w2, None, padding=1)
-            self._epilogue(z, b2, a, z, stream)
-            a = z
-        check(self.lib.uttt_nn_heads(_p(a), _p(self.heads), n, _p(self.policy), _p(self.value),
-                                     1 if softmax else 0, ctypes.c_void_p(stream)))
-        return self.policy[:n], self.value[:n]
+        check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(self.buf[0])))
+        return self._tower_heads(n, softmax)
 
-    def _forward_wino(self, n, softmax):
-        stream = ctypes.c_void_p(torch.cuda.current_stream(self.engine.device).cuda_stream)
+    @torch.no_grad()
+    def forward_states(self, states, softmax=True):
+        """Evaluate packed states (a STATE_DTYPE numpy array, any count <= max_batch)."""
+        import numpy as np
+        n = len(states)
+        if n > self.max_batch:
+            raise ValueError(f"{n} states > max_batch {self.max_batch}")
+        if self.states is None:
+            self.states = torch.zeros((self.max_batch, 8), dtype=torch.int32, device=self.device)
+        if n == 0:
+            return self.policy[:0], self.value[:0]
+        st = np.ascontiguousarray(states).view(np.int32).reshape(n, 8)
+        self.states[:n].copy_(torch.from_numpy(st))
+        check(self.lib.uttt_nn_stem_states(_p(self.states), n, _p(self.stem_w), _p(self.stem_b), _p(self.buf[0]),
+                                           self._stream()))
+        return self._tower_heads(n, softmax)
+
+    def _tower_heads(self, n, softmax):
+        stream = self._stream()
         x, t, y = self.buf
-        check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(x)))
         if self.conv == "wino3h":
-            if self.amax_pos == self.AMAX_RING:
-                self.amax.view(torch.float32).zero_()[::self.amax_stride] = self.stem_bound
-                self.amax_pos = 0
-            base = self.amax.data_ptr() + 4 * self.amax_stride * self.amax_pos
-            self.amax_pos += 1
-            slot = lambda i: ctypes.c_void_p(base + 4 * i)  # noqa: E731
             fn = self.lib.uttt_nn_conv3x3_wino3h
-            for i, ((u1, s1, b1), (u2, s2, b2)) in enumerate(self.wino):
-                check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), slot(2 * i), slot(2 * i + 1), n,
-                         stream))
-                check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), slot(2 * i + 1), slot(2 * i + 2),
-                         n, stream))
+            rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
+            cap = self.max_batch
+            i = 0
+            for (u1, s1, b1), (u2, s2, b2) in self.wino:
+                src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
+                check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), src[0], src[1], rows[i % 4],
+                         rows[(i + 1) % 4], cap, n, stream))
+                i += 1
+                check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), rows[(i - 1) % 4], 1, rows[i % 4],
+                         rows[(i + 1) % 4], cap, n, stream))
+                i += 1
                 x, y = y, x
-            check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
-                                         1 if softmax else 0, stream))
-            return self.policy[:n], self.value[:n]
-        for u1, b1, u2, b2 in self.wino:
-            check(self.conv_fn(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
-            check(self.conv_fn(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
-            x, y = y, x
+        else:
+            fn = self.lib.uttt_nn_conv3x3_wino3
+            for (u1, _, b1), (u2, _, b2) in self.wino:
+                check(fn(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
+                check(fn(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
+                x, y = y, x
         check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
                                      1 if softmax else 0, stream))
         return self.policy[:n], self.value[:n]
 
     def __call__(self, x, n):
         return self.forward(n, True)
-
-
-def wino_weights(w):
-    """Folded conv weight (128,128,3,3) -> Winograd U (16,128,128) [xi][ci][co] (host, double precision)."""
-    import numpy as np
-    wc = np.ascontiguousarray(w.detach().float().cpu().numpy())
-    u = np.zeros((16, 128, 128), np.float32)
-    lib = _lib.load()
-    check(lib.uttt_nn_wino_weights(wc.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-                                   u.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
-    return torch.from_numpy(u)
 
 
 def wino3_weights(w):
@@ -220,24 +228,68 @@ def amax(x, out=None):
     return out
 
 
-def conv3x3_wino3h(x, u, su, bias, residual=None, y_amax=None):
+def board_amax(x):
+    """Per-board max |x| of (n,81,128) activations as int32 float bits (the y_amax row form)."""
+    return x.abs().reshape(x.shape[0], -1).amax(dim=1).contiguous().view(torch.int32)
+
+
+def conv3x3_wino3h(x, u, su, bias, residual=None, y_amax=None, x_amax=None):
     """Test/utility wrapper for the split-f16 F(3x3,3x3) kernel: x (n,81,128) f32 cuda ->
-    relu(conv3x3(x) + bias (+ residual)); u, su from wino3h_weights()."""
+    relu(conv3x3(x) + bias (+ residual)); u, su from wino3h_weights(). x_amax: per-board
+    max rows (default: computed from x); y_amax: optional (n,) int32 row receiving max(y) per board."""
     y = torch.empty_like(x)
-    xa = amax(x)
+    xa = board_amax(x) if x_amax is None else x_amax
     check(_lib.load().uttt_nn_conv3x3_wino3h(_p(x), _p(u), ctypes.c_float(su), _p(bias),
-                                             _p(residual) if residual is not None else None, _p(y), _p(xa),
-                                             _p(y_amax) if y_amax is not None else None, x.shape[0],
+                                             _p(residual) if residual is not None else None, _p(y), _p(xa), 1,
+                                             _p(y_amax) if y_amax is not None else None, None, 0, x.shape[0],
                                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return y
 
 
-def conv3x3_wino(x, u, bias, residual=None, f3=False):
-    """Test/utility wrapper: x (n,81,128) f32 cuda -> relu(conv3x3(x) + bias (+ residual)).
-    f3: u is a wino3_weights() transform (F(3x3,3x3) kernel), else wino_weights() (F(2x2,3x3))."""
+def conv3x3_wino3(x, u, bias, residual=None):
+    """Test/utility wrapper: x (n,81,128) f32 cuda -> relu(conv3x3(x) + bias (+ residual)), u from
+    wino3_weights() (the f32-MFMA F(3x3,3x3) kernel)."""
     y = torch.empty_like(x)
-    lib = _lib.load()
-    fn = lib.uttt_nn_conv3x3_wino3 if f3 else lib.uttt_nn_conv3x3_wino
-    check(fn(_p(x), _p(u), _p(bias), _p(residual) if residual is not None else None, _p(y),
-             x.shape[0], ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    check(_lib.load().uttt_nn_conv3x3_wino3(_p(x), _p(u), _p(bias), _p(residual) if residual is not None else None,
+                                            _p(y), x.shape[0], ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return y
+
+
+_DUAL_ATTRS = ("conv_input", "bn_input", "residual_blocks", "policy_conv", "policy_bn", "policy_fc", "value_conv",
+               "value_bn", "value_fc1", "value_fc2")
+
+
+def is_dual_network(model):
+    """True for a DualNetwork (this package's or the reference's dual_network.DualNetwork: same
+    module names, dual_network.py:47-87) of the shape the fused kernels compute: 128 filters,
+    3x3 convs, a multiple of 2 residual blocks, 81 policy outputs, eval mode."""
+    try:
+        if not all(hasattr(model, a) for a in _DUAL_ATTRS) or getattr(model, "training", False):
+            return False
+        if tuple(model.conv_input.weight.shape) != (128, 3, 3, 3):
+            return False
+        blocks = list(model.residual_blocks)
+        if not blocks or (2 * len(blocks)) % FusedNetworkEvaluator.NROW:
+            return False
+        for b in blocks:
+            if tuple(b.conv1.weight.shape) != (128, 128, 3, 3) or tuple(b.conv2.weight.shape) != (128, 128, 3, 3):
+                return False
+        return (tuple(model.policy_fc.weight.shape) == (81, 162) and tuple(model.value_fc1.weight.shape) == (256, 81)
+                and tuple(model.value_fc2.weight.shape) == (1, 256))
+    except (AttributeError, TypeError):
+        return False
+
+
+def evaluator_kind(model, kind=None):
+    """Which leaf evaluator the drop-ins use for `model`: "fused" (the HIP kernels, default for
+    a DualNetwork), or "torch" (model(x) under PyTorch-ROCm: any other callable, or forced by
+    kind="torch" / the environment variable UTTT_EVALUATOR=torch)."""
+    import os
+    kind = kind or os.environ.get("UTTT_EVALUATOR", "auto")
+    if kind not in ("auto", "fused", "torch"):
+        raise ValueError("evaluator kind must be 'auto', 'fused' or 'torch'")
+    if kind == "auto":
+        return "fused" if is_dual_network(model) else "torch"
+    if kind == "fused" and not is_dual_network(model):
+        raise ValueError("the fused evaluator needs a DualNetwork (128 filters, 3x3, eval mode)")
+    return kind

@@ -53,6 +53,15 @@ class NetworkEvaluator:
         return p[:n].float(), v[:n].float()
 
 
+def model_evaluator_factory(model, kind=None):
+    """make(engine) -> evaluator for a model: the fused HIP evaluator for a DualNetwork (the
+    drop-ins' default, nnfast.evaluator_kind), else the model called on the engine's NCHW batch."""
+    from .nnfast import FusedNetworkEvaluator, evaluator_kind
+    if evaluator_kind(model, kind) == "fused":
+        return lambda eng: FusedNetworkEvaluator(model, eng)
+    return lambda eng: NetworkEvaluator(model, eng.max_trees)
+
+
 class BatchedSearch:
     """pv_mcts_scores (uttt_mcts.cpp:84-196) for many root states at once."""
 
@@ -119,7 +128,7 @@ class SelfPlay:
     last waves on the GPU. Records are unchanged (each game depends only on its id)."""
 
     def __init__(self, slots, evaluate_count=50, batch_size=8, temperature=1.0, device=None, evaluator=None,
-                 model=None, cache_log2=None, cache_clear_every=32, lanes=1):
+                 model=None, cache_log2=None, cache_clear_every=32, lanes=1, evaluator_kind=None):
         if lanes < 1 or slots % lanes:
             raise ValueError("slots must be a positive multiple of lanes")
         per = slots // lanes
@@ -138,7 +147,7 @@ class SelfPlay:
         self.batch_size = batch_size
         self.temperature = temperature
         if evaluator is None and model is not None:
-            self.set_evaluator(lambda eng: NetworkEvaluator(model, eng.max_trees))
+            self.set_evaluator(model_evaluator_factory(model, evaluator_kind))
         elif evaluator is None:
             self.set_evaluator(HashEvaluator)
         else:
@@ -269,6 +278,12 @@ class SelfPlay:
         return out
 
 
+def default_lanes(slots):
+    """Lanes the drop-ins use: two engines on two streams once the per-lane batch stays large
+    (Lanes), one below that."""
+    return 2 if slots >= 1024 and slots % 2 == 0 else 1
+
+
 def history_from_records(records):
     """The reference .history schema (self_play_cpp.py:59, :95-99): a flat list of
     [input (9,9,3) f32, policy (81,) f64, value int] over games in id order."""
@@ -280,4 +295,4 @@ def history_from_records(records):
 
 
 __all__ = ["BatchedSearch", "SelfPlay", "HashEvaluator", "NetworkEvaluator", "history_from_records",
-           "initial_states"]
+           "initial_states", "model_evaluator_factory", "default_lanes"]
