@@ -80,6 +80,8 @@ int uttt_state_is_done(const uttt_state_t *s);
 int uttt_state_is_first_player(const uttt_state_t *s);
 /* to_input_tensor — cpp/uttt_game.cpp:244-280 (HWC (9,9,3) flat) */
 void uttt_state_input_hwc(const uttt_state_t *s, float out[243]);
+/* The same for n states (out: n x 243 floats), e.g. the rank-0 .history build after a gather. */
+int uttt_states_input_hwc(const uttt_state_t *s, int64_t n, float *out);
 /* to_string — cpp/uttt_game.cpp:194-241; returns length, or -(needed) if cap too small */
 int uttt_state_to_string(const uttt_state_t *s, char *buf, int32_t cap);
 /* boltzman — cpp/uttt_mcts.cpp:199-216 */

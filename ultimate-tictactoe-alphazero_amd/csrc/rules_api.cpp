@@ -101,6 +101,15 @@ void uttt_state_input_hwc(const uttt_state_t *s, float out[243]) {
     }
 }
 
+int uttt_states_input_hwc(const uttt_state_t *s, int64_t n, float *out) {
+    if ((!s || !out) && n > 0) {
+        set_error("uttt_states_input_hwc: null pointer");
+        return UTTT_ERR_ARG;
+    }
+    for (int64_t i = 0; i < n; ++i) uttt_state_input_hwc(s + i, out + 243 * i);
+    return UTTT_OK;
+}
+
 int uttt_state_to_string(const uttt_state_t *s, char *buf, int32_t cap) {
     // Layout of cpp/uttt_game.cpp:194-241 (board rows, main-board status, side, active board).
     const char *ox = is_first_player(*s) ? "ox" : "xo";

@@ -54,6 +54,7 @@ SIGNATURES = {
     "uttt_state_is_done": (ctypes.c_int, [_SP]),
     "uttt_state_is_first_player": (ctypes.c_int, [_SP]),
     "uttt_state_input_hwc": (None, [_SP, _F32P]),
+    "uttt_states_input_hwc": (ctypes.c_int, [_SP, _I64, _F32P]),
     "uttt_state_to_string": (ctypes.c_int, [_SP, ctypes.c_char_p, _I32]),
     "uttt_boltzman": (ctypes.c_int, [_F32P, _I32, _F32, _F32P]),
     "uttt_engine_create": (ctypes.c_int, [_I32, _I32, _I32, ctypes.POINTER(_P)]),

@@ -82,29 +82,78 @@ def gather_records(records, dst=0, group=None):
 
 
 def records_to_inputs(records):
-    """Add the (9,9,3) input tensors (uttt_game.cpp:244-280) from the packed states, on the host rules."""
+    """Add the (9,9,3) input tensors (uttt_game.cpp:244-280) from the packed states, on the host rules
+    (one batched call for all plies)."""
     import ctypes
 
     from . import _lib
     lib = _lib.load()
+    if not records:
+        return records
+    st = np.ascontiguousarray(np.concatenate([r["states"] for r in records]))
+    x = np.zeros((len(st), 243), np.float32)
+    _lib.check(lib.uttt_states_input_hwc(st.ctypes.data_as(ctypes.POINTER(_lib.UtttState)), len(st),
+                                         x.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    o = 0
     for r in records:
-        st = np.ascontiguousarray(r["states"])
-        x = np.zeros((len(st), 243), np.float32)
-        for i in range(len(st)):
-            lib.uttt_state_input_hwc(st[i:i + 1].ctypes.data_as(ctypes.POINTER(_lib.UtttState)),
-                                     x[i].ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
-        r["inputs"] = x.reshape(len(st), 9, 9, 3)
+        k = len(r["states"])
+        r["inputs"] = x[o:o + k].reshape(k, 9, 9, 3)
+        o += k
     return records
 
 
-def self_play_sharded(model, n_games, slots, seed_base, evaluate_count=50, batch_size=8, temperature=1.0):
-    """Run this rank's shard of [0, n_games) and gather to rank 0 (returns records on rank 0)."""
+def init_from_env():
+    """(rank, world, local_rank) from torchrun's environment; initialises the default process
+    group when WORLD_SIZE > 1 (RCCL on a GPU, gloo otherwise; UTTT_DIST_BACKEND overrides)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world <= 1:
+        return 0, 1, local
+    if torch.cuda.is_available():
+        local = local % torch.cuda.device_count()  # more ranks than GPUs: ranks share them
+        torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        backend = os.environ.get("UTTT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend)
+    return dist.get_rank(), dist.get_world_size(), local
+
+
+def broadcast_int(value, src=0):
+    """One Python int from `src` to every rank (the shared seed_base)."""
+    import torch
+    import torch.distributed as dist
+    backend = dist.get_backend()
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(value) if value is not None else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(t, src)
+    return int(t.item())
+
+
+def self_play_sharded(model, n_games, slots, seed_base, evaluate_count=50, batch_size=8, temperature=1.0,
+                      lanes=None, progress=None, evaluator_kind=None):
+    """Run this rank's contiguous shard of game ids [0, n_games) and gather every rank's records to
+    rank 0 (records with inputs on rank 0, None elsewhere). Game g plays from RandomState(seed_base + g)
+    whatever the world size, so the gathered records equal a single-GPU run."""
+    import torch
     import torch.distributed as dist
 
-    from .selfplay import SelfPlay
+    from .selfplay import SelfPlay, default_lanes
     rank, world = dist.get_rank(), dist.get_world_size()
     b, e = shard(n_games, rank, world)
-    sp = SelfPlay(max(1, min(slots, e - b)), evaluate_count, batch_size, temperature, model=model)
-    sp.run(b, e, seed_base)
-    recs = gather_records(sp.records(with_inputs=False))
-    return records_to_inputs(recs) if recs is not None else None
+    recs = []
+    if e > b:
+        n_slots = max(1, min(slots, e - b))
+        n_lanes = default_lanes(n_slots) if lanes is None else lanes
+        if n_slots % n_lanes:
+            n_lanes = 1
+        dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+        sp = SelfPlay(n_slots, evaluate_count, batch_size, temperature, device=dev, model=model, lanes=n_lanes,
+                      evaluator_kind=evaluator_kind)
+        sp.run(b, e, seed_base, progress)
+        recs = sp.records(with_inputs=False)
+    out = gather_records(recs)
+    return records_to_inputs(out) if out is not None else None
