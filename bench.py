@@ -3,19 +3,24 @@
 
 A step = one move of every concurrent game on this GPU: each game's search
 runs `sims` simulations (uttt_mcts.cpp:109 iterations) with the leaf
-evaluator = DualNetwork 128f x16 (random init, torch.manual_seed(0), fp32,
-PyTorch-ROCm), then the move is sampled and recorded on device. Finished games
-are replaced by new ones, so every step keeps `games` trees in flight.
+evaluator = DualNetwork 128f x16 (random init, torch.manual_seed(0): the
+network the reference's dual_network() writes as best.pth), then the move is
+sampled and recorded on device. Finished games are replaced by new ones, so
+every step keeps `games` trees in flight.
 
   python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; games sharded, no collective
-                                                       on the data path — weak scaling)
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU; games sharded by global id in
+                                                       contiguous blocks, no collective on the data path)
 
-Prints one JSON line (rank 0) with the select-kernel roofline (algorithmic
-bytes / HIP-event time on the engine's stream) and the reference's own C++
-search timed on the host cores (cpu_baseline).
+Rank 0 prints ONE JSON line: the headline (BASELINE.json's 4096 x 50 config), the
+roofline of the dominant kernel (the residual-tower conv, MFMA), the north star's
+select and backup kernels against HBM, and - at N=1 - extra configurations
+(`variants`: non-saturated network, evaluation cache off, C3 4096 x 400) and
+the CPU baselines (`cpu_baseline`: the reference's own C++ search with its
+DualNetwork on the host cores; `cpu_baselines`: BASELINE.md's B-tree and B-e2e).
 """
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -26,22 +31,18 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "ultimate-tictactoe-alphazero_amd")
 METRIC = "MCTS simulations/sec (whole node), 4096 games × 50 sims/move; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 (vector = matrix) peak
+F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense
+FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 MFMA (= vector) peak
+NETCAL = os.path.join(REPO, "tests", "golden", "netcal.npz")
 
-
-def select_traffic(trees_per_launch):
-    """HBM bytes per k_select launch from the committed PMC summary (tools/pmc_select.sh ->
-    tools/pmc_summary.py; FETCH_SIZE + WRITE_SIZE, separate passes, raw - see that file),
-    when it was taken at this launch size; else None. A live bench run cannot read PMC."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "pmc_select.json")), reverse=True):
-        with open(f) as fh:
-            d = json.load(fh)
-        if d.get("trees_per_launch") == trees_per_launch:
-            return {"bytes_per_launch": round(d["traffic_bytes_raw"]),
-                    "read_bytes": round(d["fetch_bytes"]), "write_bytes": round(d["write_bytes"]),
-                    "source": os.path.relpath(f, REPO)}
-    return None
+# residual-tower conv, per board: MFMA flops the kernels issue, and the direct 3x3 conv's flops
+CONV_EXEC_FLOP = {"wino3h": 3 * 9 * 25 * 128 * 128 * 2,   # F(3x3,3x3): 9 tiles x 25 points, 3 f16 products
+                  "wino3": 9 * 25 * 128 * 128 * 2}        # the same on the f32 MFMA, 1 product
+CONV_DIRECT_FLOP = 2 * 81 * 128 * 1152
+CONV_PEAK = {"wino3h": F16_DENSE_PEAK_TFLOPS, "wino3": FP32_PEAK_TFLOPS}
+# residual-tower conv, algorithmic HBM bytes per board: read x, write y (+ read the residual on
+# every second conv); the transformed weights (1.6 MB) are read once per launch, L2/MALL-resident
+CONV_BYTES_PER_BOARD = 81 * 128 * 4 * 2.5
 
 
 def nn_macs():
@@ -52,9 +53,6 @@ def nn_macs():
 
 
 NN_FLOP_PER_STATE = 2 * nn_macs()  # 0.765 GFLOP per evaluated position
-# residual-tower MFMA flops actually executed per board / direct-equivalent flops per state
-TOWER_MFMA_FRACTION = {"fused": 3 * 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE,      # F(3x3,3x3), 3 f16 products
-                       "fused-f32": 32 * 9 * 25 * 128 * 128 * 2 / NN_FLOP_PER_STATE}      # F(3x3,3x3), f32
 
 
 def parse():
@@ -65,103 +63,120 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "fused-f32", "nn", "nn-plain", "hash"],
-                    default="fused")
+    ap.add_argument("--evaluator", choices=["fused", "fused-f32", "nn", "hash"], default="fused")
+    ap.add_argument("--net", choices=["seed0", "calibrated"], default="seed0",
+                    help="seed0: the reference's initial best.pth; calibrated: tests/golden/netcal.npz")
     ap.add_argument("--age", type=int, default=100,
                     help="moves played before warmup so the timed population mixes all game phases")
-    ap.add_argument("--cudnn-benchmark", type=int, default=1)
     ap.add_argument("--lanes", type=int, default=2,
                     help="engines per GPU, each on its own stream; their network evaluations overlap")
     ap.add_argument("--cache-log2", type=int, default=21, help="evaluation cache entries (log2); 0 = off")
-    ap.add_argument("--tag", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--cpu-baseline-child", choices=["cpu-nn", "tree", "device-nn"], help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
-# ------------------------------------------------------------- CPU baseline --
-def cpu_baseline_child(seconds):
-    """Reference C++ PV-MCTS (oracle/_ref: cpp/uttt_game.cpp + uttt_mcts.cpp + python_bindings.cpp
-    compiled from the reference sources) driven like self_play_cpp.play, leaf evaluator = the same
-    DualNetwork on the host cores (torch CPU fp32). Falls back to the C oracle port if _ref is absent."""
-    import numpy as np
-    import torch
+def newest_profile(name, match):
+    """The newest committed profiles/r*/<name> JSON whose fields equal `match` (PMC summaries:
+    a live bench cannot read counters)."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", name)), reverse=True):
+        with open(f) as fh:
+            d = json.load(fh)
+        if all(d.get(k) == v for k, v in match.items()):
+            d["source"] = os.path.relpath(f, REPO)
+            return d
+    return None
 
-    sys.path.insert(0, PKG)
-    from uttt_amd.model import random_network
 
-    net = random_network(0, "cpu")
-    threads = torch.get_num_threads()
+# ------------------------------------------------------------- CPU baselines --
+def _ref_uttt():
+    """The reference's own uttt_cpp (oracle/_ref, compiled from its sources by oracle/Makefile)."""
     ref_dir = os.path.join(REPO, "oracle", "_ref")
-    kind = "reference"
-    try:
-        sys.path.insert(0, ref_dir)
-        import uttt_cpp as ref_uttt  # the reference's own module, built from its sources
-        assert os.path.dirname(os.path.abspath(ref_uttt.__file__)) == ref_dir
-    except Exception:
-        kind = "port"
-        ref_uttt = None
+    sys.path.insert(0, ref_dir)
+    import uttt_cpp as ref_uttt
+    assert os.path.dirname(os.path.abspath(ref_uttt.__file__)) == ref_dir
+    return ref_uttt
+
+
+def _serial_selfplay(ref_uttt, infer, seconds, rng):
+    """self_play_cpp.play's loop (self_play_cpp.py:47-93) on the reference search: moves until the
+    time is up, games restarted as they end. Returns (sims, moves, seconds)."""
+    import numpy as np
+    sims = moves = 0
+    state = ref_uttt.State()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        if state.is_done():
+            state = ref_uttt.State()
+        sc = np.array(ref_uttt.pv_mcts_scores(model=infer, state=state, temperature=1.0, evaluate_count=50,
+                                              batch_size=8), np.float64)
+        legal = state.legal_actions()
+        sc = sc / np.sum(sc)
+        state = state.next(int(rng.choice(legal, p=sc)))
+        sims += 50
+        moves += 1
+    return sims, moves, time.perf_counter() - t0
+
+
+def cpu_baseline_child(kind, seconds):
+    import numpy as np
+
+    sys.path[:0] = [REPO, PKG]
+    if kind == "tree":
+        # B-tree (BASELINE.md §3): the reference's C++ search alone (hash evaluator, no network),
+        # one game per process on the box's host cores
+        import multiprocessing as mp
+        from oracle import ref as refdrv
+        procs = max(1, min(16, os.cpu_count() or 1))
+        moves = max(200, int(seconds * 3000))
+        with mp.get_context("fork").Pool(procs) as pool:
+            t0 = time.perf_counter()
+            res = pool.starmap(refdrv.bench_tree, [(50, 8, moves)] * procs)
+            dt = time.perf_counter() - t0
+        # the processes run concurrently: the node's rate is the sum of their own rates
+        print(json.dumps({"value": round(sum(r for r, _ in res), 1), "unit": "simulations/s", "cores": procs,
+                          "kind": "reference",
+                          "sample": f"{procs} processes x {moves} consecutive 50-sim moves (MCTS_BATCH_SIZE 8) of the "
+                                    f"reference's C++ search with the deterministic hash evaluator, {dt:.1f} s",
+                          "per_core": round(float(np.mean([r for r, _ in res])), 1)}))
+        return
+    import torch
+    from uttt_amd.model import random_network
+    ref_uttt = _ref_uttt()
+    if kind == "cpu-nn":
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", 0)
+    net = random_network(0, dev)
+    threads = torch.get_num_threads()
 
     def infer(states):  # pv_mcts_cpp.py:37-78 glue
         x = np.stack([np.asarray(s.to_input_tensor(), np.float32).reshape(9, 9, 3) for s in states])
-        x = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 3, 1, 2)))
+        x = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 3, 1, 2))).to(dev)
         with torch.no_grad():
             p, v = net(x)
-        p, v = p.numpy(), v.numpy()
+        p, v = p.cpu().numpy(), v.cpu().numpy()
         return [(p[i], float(v[i][0])) for i in range(len(states))]
 
-    rng = np.random.RandomState(1234)
-    sims = moves = 0
-    tree_only = None
-    t0 = time.perf_counter()
-    if ref_uttt is not None:
-        state = ref_uttt.State()
-        while time.perf_counter() - t0 < seconds:
-            if state.is_done():
-                state = ref_uttt.State()
-            sc = np.array(ref_uttt.pv_mcts_scores(model=infer, state=state, temperature=1.0, evaluate_count=50,
-                                                  batch_size=8), np.float64)
-            legal = state.legal_actions()
-            sc = sc / np.sum(sc)
-            state = state.next(int(rng.choice(legal, p=sc)))
-            sims += 50
-            moves += 1
-        dt = time.perf_counter() - t0
-        from oracle import ref as refdrv
-        if refdrv.available():
-            tree_only, _ = refdrv.bench_tree(50, 8, 2000)
-    else:
-        from oracle import core
-        s = core.OrState.initial()
-
-        def ev(x):
-            with torch.no_grad():
-                p, v = net(torch.from_numpy(np.asarray(x, np.float32).reshape(1, 3, 9, 9)))
-            return p.numpy()[0], float(v.numpy()[0, 0])
-
-        while time.perf_counter() - t0 < seconds:
-            if s.is_done():
-                s = core.OrState.initial()
-            sc, _, _ = core.pv_mcts_scores(s, 1.0, 50, 8, ev)
-            legal = s.legal_actions()
-            s = s.next(legal[int(np.argmax(sc))])
-            sims += 50
-            moves += 1
-        dt = time.perf_counter() - t0
-    print(json.dumps({"value": sims / dt, "unit": "simulations/s", "cores": threads, "kind": kind,
-                      "sample": f"{moves} consecutive self-play moves (50 sims, MCTS_BATCH_SIZE 8, tau 1) of "
-                                f"the reference C++ search + DualNetwork fp32 on {threads} CPU threads, "
-                                f"{dt:.1f} s",
-                      "tree_only_1core": tree_only}))
+    if kind == "device-nn":
+        _serial_selfplay(ref_uttt, infer, 2.0, np.random.RandomState(0))  # MIOpen / allocator warmup
+    sims, moves, dt = _serial_selfplay(ref_uttt, infer, seconds, np.random.RandomState(1234))
+    where = f"DualNetwork fp32 on {threads} CPU threads" if kind == "cpu-nn" else \
+        "DualNetwork fp32 on the MI355X (PyTorch-ROCm, one flush of <= 8 states per call)"
+    print(json.dumps({"value": sims / dt, "unit": "simulations/s", "cores": threads if kind == "cpu-nn" else 1,
+                      "kind": "reference",
+                      "sample": f"{moves} consecutive self-play moves (50 sims, MCTS_BATCH_SIZE 8, tau 1) of the "
+                                f"reference's C++ search (oracle/_ref, built from its sources) + {where}, {dt:.1f} s"}))
 
 
-def run_cpu_baseline(seconds):
-    env = dict(os.environ)
-    env["HIP_VISIBLE_DEVICES"] = ""
-    env["CUDA_VISIBLE_DEVICES"] = ""
-    env["PYTHONPATH"] = REPO
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--cpu-seconds",
+def run_cpu_baseline(kind, seconds):
+    env = dict(os.environ, PYTHONPATH=REPO)
+    if kind != "device-nn":
+        env["HIP_VISIBLE_DEVICES"] = ""
+        env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", kind, "--cpu-seconds",
                         str(seconds)], capture_output=True, text=True, env=env, cwd=REPO, timeout=seconds * 20 + 300)
     for line in reversed(r.stdout.strip().splitlines()):
         if line.startswith("{"):
@@ -170,19 +185,167 @@ def run_cpu_baseline(seconds):
 
 
 # ----------------------------------------------------------------- GPU bench --
+def union_ms(intervals):
+    busy, cur = 0.0, None
+    for lo, hi in sorted(intervals):
+        if cur is None or lo > cur[1]:
+            if cur is not None:
+                busy += cur[1] - cur[0]
+            cur = [lo, hi]
+        else:
+            cur[1] = max(cur[1], hi)
+    return busy + (cur[1] - cur[0] if cur is not None else 0.0)
+
+
+def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, age, warmup, steps, evaluator):
+    """Continuous self-play of `games` slots on this GPU; returns the timed-window statistics."""
+    import torch
+    import torch.distributed as dist
+    from uttt_amd import HashEvaluator, NetworkEvaluator, SelfPlay
+    from uttt_amd.distributed import shard
+    from uttt_amd.model import FoldedDualNetwork
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+
+    dev = torch.device("cuda", local)
+    sp = SelfPlay(games, sims, batch, 1.0, device=local, cache_log2=cache_log2, lanes=lanes)
+    conv = {"fused": "wino3h", "fused-f32": "wino3"}.get(evaluator)
+    tower_events = []
+    if evaluator == "hash":
+        make_inner = HashEvaluator
+    elif conv:
+        def make_inner(eng):
+            fe = FusedNetworkEvaluator(net, eng, conv=conv)
+            fe.tower_events = tower_events
+            return fe
+    else:
+        folded = FoldedDualNetwork(net).to(dev)
+        make_inner = lambda eng: NetworkEvaluator(folded, eng.max_trees)  # noqa: E731
+    ev_pairs = []
+    rows = [0]
+
+    def make_timed(eng):
+        inner = make_inner(eng)
+
+        def timed_eval(x, n):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            out = inner(x, n)
+            b.record()
+            ev_pairs.append((a, b))
+            rows[0] += n
+            return out
+
+        timed_eval.needs_input = getattr(inner, "needs_input", True)
+        return timed_eval
+
+    sp.set_evaluator(make_timed)
+    # continuous self-play: rank r owns the contiguous block r of global game ids (the same
+    # scheme as self_play_cpp's torchrun sharding), large enough for every game it can start
+    per_rank = (age + warmup + steps + 2) * games
+    gb, ge = shard(per_rank * world, rank, world)
+    sp.begin(gb, ge, 1234, arena_plies=per_rank)
+    for _ in range(age + warmup):
+        sp.step()
+    torch.cuda.synchronize()
+    ev_pairs.clear()
+    tower_events.clear()
+    rows[0] = 0
+    sp.reset_stats()
+    sp.set_timing(True)
+    rounds0, finished0 = sp.rounds, sp.finished
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    base = torch.cuda.Event(enable_timing=True)
+    base.record()
+    t0 = time.perf_counter()
+    done = 0
+    for _ in range(steps):
+        done += sp.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    ivs = [(base.elapsed_time(a), base.elapsed_time(b)) for a, b in ev_pairs]
+    tower = [(n, a.elapsed_time(b)) for n, a, b in tower_events]
+    st = {k: sp.kernel_stats(k) for k in ("select", "apply", "scan", "move_end", "select_levels", "select_trees",
+                                          "select_max_levels_sum")}
+    out = {"sims": done, "elapsed": elapsed, "rows": rows[0], "nn_ms": union_ms(ivs),
+           "nn_lane_sum_ms": sum(hi - lo for lo, hi in ivs), "tower": tower, "stats": st,
+           "rounds": sp.rounds - rounds0, "finished": sp.finished - finished0, "conv": conv,
+           "cache": sp.cache_stats() if cache_log2 else None, "trees_per_launch": games // lanes}
+    del sp
+    torch.cuda.empty_cache()
+    return out
+
+
+def summarize(r, steps):
+    """Compact statistics of one run_config result (rank-local)."""
+    out = {"value": round(r["sims"] / r["elapsed"], 1), "ms_per_step": round(r["elapsed"] / steps * 1e3, 3),
+           "nn_share_of_step": round(r["nn_ms"] / 1e3 / r["elapsed"], 4), "rows_per_step": round(r["rows"] / steps, 1),
+           "rounds_per_step": round(r["rounds"] / steps, 2)}
+    if r["cache"]:
+        c = r["cache"]
+        out["eval_cache_hit_rate"] = round(c["hits"] / max(c["hits"] + c["misses"], 1), 4)
+    return out
+
+
+def conv_roofline(r):
+    """The dominant kernel: one residual-tower conv launch. achieved = executed MFMA flops per launch
+    / the launch's average duration, from HIP events recorded on the lane's stream around each forward's
+    32 launches (so the few-us launch gaps are included: conservative)."""
+    conv = r["conv"]
+    if not conv or not r["tower"]:
+        return None
+    ncv = 32
+    boards = sum(n for n, _ in r["tower"])
+    ms = sum(t for _, t in r["tower"])
+    launches = ncv * len(r["tower"])
+    avg_us = ms * 1e3 / launches
+    boards_per_launch = boards / len(r["tower"])
+    flop = CONV_EXEC_FLOP[conv] * boards_per_launch
+    achieved = flop / (avg_us * 1e-6) / 1e12
+    pmc = newest_profile("pmc_conv.json", {"kernel": "k_wino3h_conv"}) if conv == "wino3h" else None
+    traffic = round(pmc["hbm_bytes_per_board"] * boards_per_launch) if pmc else None
+    algo_bytes = CONV_BYTES_PER_BOARD * boards_per_launch + 25 * 128 * 128 * (4 if conv == "wino3h" else 4)
+    return {"kernel": f"k_{conv}_conv (residual-tower 3x3 conv, Winograd F(3x3,3x3) on the "
+                      f"{'f16 MFMA, 3-term split-f16 products, f32 accumulation' if conv == 'wino3h' else 'f32 MFMA'})",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": CONV_PEAK[conv], "unit": "TFLOP/s",
+            "frac": round(achieved / CONV_PEAK[conv], 4), "traffic": traffic,
+            "traffic_detail": ({k: pmc[k] for k in ("hbm_bytes_per_board", "fetch_bytes_per_board_x2",
+                                                    "write_bytes_per_board", "source") if k in pmc} if pmc else None),
+            "algo_hbm_bytes_per_launch": round(algo_bytes),
+            "avg_launch_us": round(avg_us, 2), "launches": launches, "boards_per_launch": round(boards_per_launch, 1),
+            "executed_flop_per_board": CONV_EXEC_FLOP[conv], "direct_equiv_flop_per_board": CONV_DIRECT_FLOP,
+            "direct_equiv_tflops": round(CONV_DIRECT_FLOP * boards_per_launch / (avg_us * 1e-6) / 1e12, 1),
+            "note": "two lanes' conv launches overlap on the GPU, so each launch's duration includes the time it "
+                    "shares the CUs with the other lane's; aggregate = nn.mfma_executed_tflops"}
+
+
+def hbm_roofline(name, stat, trees_per_launch, pmc_name=None):
+    ms, launches, byts = stat["ms"], max(stat["launches"], 1), stat["bytes"]
+    achieved = (byts / 1e9) / (ms / 1e3) if ms > 0 else 0.0
+    pmc = newest_profile(pmc_name, {"trees_per_launch": trees_per_launch}) if pmc_name else None
+    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": round(pmc["traffic_bytes_raw"]) if pmc else None,
+            "traffic_detail": ({"read_bytes": round(pmc["fetch_bytes"]), "write_bytes": round(pmc["write_bytes"]),
+                                "source": pmc["source"]} if pmc else None),
+            "algo_bytes_per_launch": round(byts / launches), "avg_launch_us": round(ms * 1e3 / launches, 2),
+            "launches": stat["launches"]}
+
+
 def main():
     args = parse()
     if args.cpu_baseline_child:
-        cpu_baseline_child(args.cpu_seconds)
+        cpu_baseline_child(args.cpu_baseline_child, args.cpu_seconds)
         return
     import torch
     import torch.distributed as dist
 
-    sys.path.insert(0, REPO)
-    sys.path.insert(0, PKG)
-    from uttt_amd import HashEvaluator, NetworkEvaluator, SelfPlay
-    from uttt_amd.model import FoldedDualNetwork, random_network
-    from uttt_amd.nnfast import FusedNetworkEvaluator
+    sys.path[:0] = [REPO, PKG]
+    from uttt_amd.model import calibrated_network, random_network
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -191,106 +354,15 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
 
     G, S, B = args.games, args.sims, args.batch
-    net = random_network(0, dev)
-    model = FoldedDualNetwork(net).to(dev) if args.evaluator == "nn" else net
-    sp = SelfPlay(G, S, B, 1.0, device=local, cache_log2=args.cache_log2, lanes=args.lanes)
-    if args.evaluator == "hash":
-        make_inner = HashEvaluator
-    elif args.evaluator.startswith("fused"):
-        conv = {"fused": "wino3h", "fused-f32": "wino3"}[args.evaluator]
-        make_inner = lambda eng: FusedNetworkEvaluator(net, eng, conv=conv)  # noqa: E731
-    else:
-        make_inner = lambda eng: NetworkEvaluator(model, eng.max_trees)  # noqa: E731
+    net0 = random_network(0, dev) if args.net == "seed0" else calibrated_network(NETCAL, dev)
+    r = run_config(net0, local, rank, world, G, S, B, args.lanes, args.cache_log2, args.age, args.warmup, args.steps,
+                   args.evaluator)
 
-    # NN timing: events around every evaluation on the stream it runs on (lanes
-    # overlap, so busy time is the union of the intervals), and useful rows
-    nn_stats = {"ms": 0.0, "rows": 0, "padded_rows": 0}
-    ev_pairs = []
-    pads = args.evaluator in ("nn", "nn-plain")
-
-    def make_timed(eng):
-        inner = make_inner(eng)
-
-        def timed_eval(x, n):
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            a.record()
-            out = inner(x, n)
-            b.record()
-            ev_pairs.append((a, b))
-            nn_stats["rows"] += n
-            if pads:
-                from uttt_amd.selfplay import _bucket
-                nn_stats["padded_rows"] += _bucket(n, eng.max_trees)
-            else:
-                nn_stats["padded_rows"] += n
-            return out
-
-        timed_eval.needs_input = getattr(inner, "needs_input", True)
-        return timed_eval
-
-    sp.set_evaluator(make_timed)
-    games_per_rank = 10**9
-    arena = (args.age + args.warmup + args.steps + 2) * G
-    sp.begin(rank * games_per_rank, (rank + 1) * games_per_rank, 1234, arena_plies=arena)
-
-    # Setup (not warmup, not timed): age the population. All games start together
-    # from the initial position; refilling finished slots with new games spreads
-    # the slots over every phase of a game (openings, middle games with wide
-    # child lists, endgames with terminal simulations) like continuous self-play.
-    for _ in range(args.age):
-        sp.step()
-    for _ in range(args.warmup):
-        sp.step()
-    torch.cuda.synchronize()
-    ev_pairs.clear()
-    nn_stats.update(ms=0.0, rows=0, padded_rows=0)
-    sp.reset_stats()
-    sp.set_timing(True)
-    rounds0, finished0 = sp.rounds, sp.finished
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    base = torch.cuda.Event(enable_timing=True)
-    base.record()
-    t0 = time.perf_counter()
-    sims = 0
-    for _ in range(args.steps):
-        sims += sp.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    torch.cuda.synchronize()
-    ivs = sorted((base.elapsed_time(a), base.elapsed_time(b)) for a, b in ev_pairs)
-    busy, cur = 0.0, None
-    for lo, hi in ivs:
-        if cur is None or lo > cur[1]:
-            if cur is not None:
-                busy += cur[1] - cur[0]
-            cur = [lo, hi]
-        else:
-            cur[1] = max(cur[1], hi)
-    if cur is not None:
-        busy += cur[1] - cur[0]
-    nn_stats["ms"] = busy
-    nn_stats["sum_ms"] = sum(hi - lo for lo, hi in ivs)
-    sel = sp.kernel_stats("select")
-    app = sp.kernel_stats("apply")
-    enc = sp.kernel_stats("encode")
-    scan = sp.kernel_stats("scan")
-    mend = sp.kernel_stats("move_end")
-    rounds = sp.rounds - rounds0
-    cache = sp.cache_stats() if args.cache_log2 else None
-
-    tot = torch.tensor([float(sims), elapsed], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(r["sims"]), r["elapsed"]], dtype=torch.float64, device=dev)
     if world > 1:
         s = tot[:1].clone()
         m = tot[1:].clone()
@@ -299,12 +371,35 @@ def main():
         tot = torch.cat([s, m])
     total_sims, max_elapsed = float(tot[0].item()), float(tot[1].item())
 
+    variants = None
+    if world == 1 and not args.no_variants and args.evaluator.startswith("fused"):
+        variants = {}
+        for key, kw in (("calibrated_net", dict(net=calibrated_network(NETCAL, dev))),
+                        ("cache_off", dict(cache_log2=0)),
+                        ("c3_4096x400", dict(sims=400, age=30, warmup=2, steps=4))):
+            cfg = dict(net=net0, games=G, sims=S, batch=B, lanes=args.lanes, cache_log2=args.cache_log2,
+                       age=args.age, warmup=3, steps=10, evaluator=args.evaluator)
+            cfg.update(kw)
+            rv = run_config(cfg["net"], local, 0, 1, cfg["games"], cfg["sims"], cfg["batch"], cfg["lanes"],
+                            cfg["cache_log2"], cfg["age"], cfg["warmup"], cfg["steps"], cfg["evaluator"])
+            sv = summarize(rv, cfg["steps"])
+            sv["config"] = {k: cfg[k] for k in ("games", "sims", "batch", "lanes", "cache_log2", "age", "steps")}
+            sv["net"] = "calibrated (tests/golden/netcal.npz)" if key == "calibrated_net" else args.net
+            sv["conv_roofline_frac"] = (conv_roofline(rv) or {}).get("frac")
+            variants[key] = sv
+
     if rank == 0:
         value = total_sims / max_elapsed
-        sel_ms = sel["ms"]
-        achieved = (sel["bytes"] / 1e9) / (sel_ms / 1e3) if sel_ms > 0 else 0.0
-        flops = NN_FLOP_PER_STATE * nn_stats["rows"]
-        nn_tflops = flops / (nn_stats["ms"] / 1e3) / 1e12 if nn_stats["ms"] > 0 else 0.0
+        st = r["stats"]
+        flops_direct = NN_FLOP_PER_STATE * r["rows"]
+        nn_direct_tflops = flops_direct / (r["nn_ms"] / 1e3) / 1e12 if r["nn_ms"] > 0 else 0.0
+        conv = r["conv"]
+        exec_tower = (CONV_EXEC_FLOP[conv] * 32 * r["rows"] / (r["nn_ms"] / 1e3) / 1e12) if conv and r["nn_ms"] else None
+        sel = st["select"]
+        sel_launches = max(sel["launches"], 1)
+        lev_trees = max(st["select_trees"]["bytes"], 1)
+        max_lev = st["select_max_levels_sum"]["bytes"] / sel_launches
+        sel_us = sel["ms"] * 1e3 / sel_launches
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -316,64 +411,66 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: self-play from the initial position, games refilled as they end; "
-                    "random-init DualNetwork (torch.manual_seed(0)); no checkpoint",
+            "dtype": {"fused": "f32 activations and accumulation; tower point GEMMs as 3-term split-f16 products "
+                               "on the f16 MFMA (f32-level accuracy: within 1e-5 of the reference's fp32 network)",
+                      "fused-f32": "f32", "nn": "f32", "hash": "f32 (hash evaluator)"}[args.evaluator],
+            "data": "synthetic: self-play from the initial position, games refilled as they end; DualNetwork "
+                    + ("random init torch.manual_seed(0) (the reference's initial best.pth)" if args.net == "seed0"
+                       else "with calibrated BatchNorm statistics (tests/golden/netcal.npz)") + "; no checkpoint",
             "config": {
                 "workload": f"{G} concurrent self-play games per GPU x {S} sims/move, MCTS_BATCH_SIZE {B}, "
                             f"tau 1.0, continuous self-play (finished games refilled; population aged "
                             f"{args.age} moves before warmup); one step = one move of every game",
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
-                "eval_cache_log2": args.cache_log2,
-                "lanes_per_gpu": args.lanes,
-                "evaluator": {"fused": "DualNetwork 128f x16, f32 activations/accumulation, BN folded; residual-tower "
-                                       "convs as a fused Winograd F(3x3,3x3) HIP kernel whose point GEMMs run as "
-                                       "3-term split-f16 products on the f16 MFMA with f32 accumulation "
-                                       "(csrc/wino3h_conv.hip; f32-level error, 1.4e-6 rel vs f64 per conv, tested "
-                                       "at 1e-5), stem/heads HIP kernels (csrc/nn_kernels.hip)",
-                              "fused-f32": "DualNetwork 128f x16 fp32, BN folded; residual-tower convs as a fused "
-                                           "Winograd F(3x3,3x3) f32-MFMA HIP kernel (csrc/wino3_conv.hip), stem/heads "
-                                           "HIP kernels (csrc/nn_kernels.hip)",
-                              "nn": "DualNetwork 128f x16 fp32, BN folded, channels-last (PyTorch-ROCm/MIOpen)",
-                              "nn-plain": "DualNetwork 128f x16 fp32 (PyTorch-ROCm/MIOpen)",
+                "eval_cache_log2": args.cache_log2, "lanes_per_gpu": args.lanes,
+                "evaluator": {"fused": "DualNetwork 128f x16 on HIP kernels: stem from bitboards, residual tower as "
+                                       "fused Winograd F(3x3,3x3) convs (csrc/wino3h_conv.hip, split-f16 MFMA, f32 "
+                                       "accumulation, per-board scaling), heads (csrc/nn_kernels.hip)",
+                              "fused-f32": "DualNetwork 128f x16 on HIP kernels, tower on the f32 MFMA "
+                                           "(csrc/wino3_conv.hip)",
+                              "nn": "DualNetwork 128f x16 fp32, BN folded, PyTorch-ROCm/MIOpen",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],
-                "parallelism": f"games sharded over {world} GPU(s), no data-path collective",
+                "parallelism": f"games sharded over {world} GPU(s) by contiguous global-id blocks, "
+                               f"no data-path collective",
             },
-            "roofline": {
-                "kernel": "k_select (PUCT descent, one wave per tree)",
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": (select_traffic(G // args.lanes) or {}).get("bytes_per_launch"),
-                "traffic_detail": select_traffic(G // args.lanes),
-                "algo_bytes_per_launch": round(sel["bytes"] / max(sel["launches"], 1)),
-                "avg_launch_us": round(sel_ms * 1e3 / max(sel["launches"], 1), 2),
-                "launches": sel["launches"],
-            },
-            "nn": {
-                "rows_evaluated": nn_stats["rows"], "rows_padded": nn_stats["padded_rows"],
-                "ms": round(nn_stats["ms"], 2), "share_of_step": round(nn_stats["ms"] / 1e3 / elapsed, 4),
-                "lane_sum_ms": round(nn_stats["sum_ms"], 2),
-                "achieved_tflops": round(nn_tflops, 2), "peak_tflops": FP32_PEAK_TFLOPS,
-                "frac": round(nn_tflops / FP32_PEAK_TFLOPS, 4),
-                "flops_basis": "direct-conv equivalent, 2 x MACs of dual_network.py per evaluated row "
-                               "(Winograd kernels execute fewer MFMA flops; see mfma_executed_tflops)",
-                "mfma_executed_tflops": (round(nn_tflops * TOWER_MFMA_FRACTION[args.evaluator], 2)
-                                         if args.evaluator in TOWER_MFMA_FRACTION else None),
-            },
-            "breakdown_ms": {"select": round(sel_ms, 2), "apply": round(app["ms"], 2), "encode": round(enc["ms"], 2),
-                             "scan": round(scan["ms"], 2), "move_end": round(mend["ms"], 2),
-                             "nn": round(nn_stats["ms"], 2), "wall": round(elapsed * 1e3, 2)},
-            "rounds_per_step": round(rounds / args.steps, 2),
-            "games_finished_in_timed_steps": int(sp.finished - finished0),
-            "eval_cache": (dict(cache, hit_rate=round(cache["hits"] / max(cache["hits"] + cache["misses"], 1), 4),
-                                log2_capacity=args.cache_log2) if cache else None),
+            "roofline": conv_roofline(r) if conv else hbm_roofline("k_select", sel, r["trees_per_launch"],
+                                                                   "pmc_select.json"),
+            "roofline_select": dict(hbm_roofline("k_select (PUCT descent, one wave per tree)", sel,
+                                                 r["trees_per_launch"], "pmc_select.json"),
+                                    latency_model={
+                                        "levels_per_tree_per_launch": round(st["select_levels"]["bytes"] / lev_trees, 2),
+                                        "slowest_tree_levels_per_launch": round(max_lev, 1),
+                                        "us_per_level_of_slowest_tree": round(sel_us / max(max_lev, 1e-9), 3),
+                                        "note": "a launch lasts as long as its slowest tree's chain of dependent "
+                                                "levels (node header -> child stats -> next node); us_per_level is "
+                                                "the launch time divided by that chain"}),
+            "roofline_backup": hbm_roofline("k_apply (expand + backup, one wave per pending leaf)", st["apply"],
+                                            r["trees_per_launch"]),
+            "nn": {"rows_evaluated": r["rows"], "ms": round(r["nn_ms"], 2),
+                   "share_of_step": round(r["nn_ms"] / 1e3 / r["elapsed"], 4),
+                   "lane_sum_ms": round(r["nn_lane_sum_ms"], 2),
+                   "mfma_executed_tflops": round(exec_tower, 2) if exec_tower else None,
+                   "frac": round(exec_tower / CONV_PEAK[conv], 4) if exec_tower else None,
+                   "peak_tflops": CONV_PEAK[conv] if conv else None,
+                   "frac_basis": "residual-tower MFMA flops actually issued (Winograd, 3 f16 products) per evaluated "
+                                 "row / union of NN-call time (stem and heads included), over the dtype's dense peak",
+                   "direct_equiv_tflops": round(nn_direct_tflops, 2),
+                   "direct_equiv_basis": "2 x MACs of dual_network.py per evaluated row (what the reference's "
+                                         "network costs as direct convs)"},
+            "breakdown_ms": {"select": round(sel["ms"], 2), "apply": round(st["apply"]["ms"], 2),
+                             "scan": round(st["scan"]["ms"], 2), "move_end": round(st["move_end"]["ms"], 2),
+                             "nn": round(r["nn_ms"], 2), "wall": round(r["elapsed"] * 1e3, 2)},
+            "rounds_per_step": round(r["rounds"] / args.steps, 2),
+            "games_finished_in_timed_steps": int(r["finished"]),
+            "eval_cache": (dict(r["cache"], hit_rate=round(r["cache"]["hits"] / max(r["cache"]["hits"] +
+                                                                                     r["cache"]["misses"], 1), 4),
+                                log2_capacity=args.cache_log2) if r["cache"] else None),
+            "variants": variants,
         }
-        if not args.no_cpu_baseline:
-            cb = run_cpu_baseline(args.cpu_seconds)
-            out["cpu_baseline"] = cb
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = run_cpu_baseline("cpu-nn", args.cpu_seconds)
+            out["cpu_baselines"] = {"b_tree_all_cores": run_cpu_baseline("tree", 10.0),
+                                    "b_e2e_nn_on_device": run_cpu_baseline("device-nn", 10.0)}
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -206,7 +206,9 @@ int uttt_engine_cache_stats(uttt_engine_t *eng, int64_t *hits, int64_t *misses, 
 /* Per-kernel timing with HIP events on the engine's stream (off by default). */
 int uttt_engine_set_timing(uttt_engine_t *eng, int32_t enabled);
 /* kernel: 0 select, 1 apply, 2 encode, 3 scan, 4 move_end, 5 hash_eval.
- * Outputs total ms, launches and algorithmic bytes. */
+ * Outputs total ms, launches and algorithmic bytes. Counters without launches
+ * (value in *algo_bytes): 6 tree levels walked by select (sum over descents of depth + 1),
+ * 7 trees that descended, 9 sum over select launches of the slowest tree's levels. */
 int uttt_engine_kernel_stats(uttt_engine_t *eng, int32_t kernel, double *total_ms, int64_t *launches,
                              int64_t *algo_bytes);
 int uttt_engine_reset_stats(uttt_engine_t *eng);

@@ -14,7 +14,7 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 from uttt_amd import _lib  # noqa: E402
 from uttt_amd.model import fold_bn, random_network  # noqa: E402
-from uttt_amd.nnfast import amax, conv3x3_wino3h, wino3_weights, wino3h_weights, _p  # noqa: E402
+from uttt_amd.nnfast import amax, board_amax, conv3x3_wino3h, wino3_weights, wino3h_weights, _p  # noqa: E402
 
 
 def timeit(fn, reps=20):
@@ -45,13 +45,14 @@ def main():
         y = torch.empty_like(x)
         xa = amax(x)
         t3 = timeit(lambda: lib.uttt_nn_conv3x3_wino3(_p(x), _p(u3), _p(b), None, _p(y), n, st))
-        th = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y), _p(xa),
-                                                      None, n, st))
+        ba = board_amax(x)
+        th = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y), _p(ba), 1,
+                                                      None, None, 0, n, st))
         r = torch.randn_like(x)
         th_res = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(r), _p(y),
-                                                          _p(xa), None, n, st))
+                                                          _p(ba), 1, None, None, 0, n, st))
         abl = {m: timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y),
-                                                                    _p(xa), n, m, st)) for m in [int(v) for v in os.environ.get("MODES", "1,2,64,16,32,48,49,112").split(",")]}
+                                                                    _p(xa), n, m, st)) for m in [int(v) for v in os.environ.get("MODES", "1,2,8,64,16,32,48,49,112,512").split(",")]}
         lib.uttt_diag_wino3h_pf.argtypes = lib.uttt_diag_wino3h_ablation.argtypes
         for pf in [int(v) for v in os.environ.get("PFS", "").split(",") if v]:
             abl["pf%d" % pf] = timeit(lambda pf=pf: lib.uttt_diag_wino3h_pf(_p(x), _p(uh), ctypes.c_float(su), _p(b),

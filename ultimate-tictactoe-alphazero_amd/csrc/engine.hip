@@ -70,7 +70,13 @@ constexpr int32_t kErrDepth = 4;
 constexpr int32_t kErrSelect = 8;
 constexpr int32_t kErrMask = kErrCapacity | kErrDepth | kErrSelect;
 
-enum KernelId { kKSelect = 0, kKApply, kKEncode, kKScan, kKMoveEnd, kKHash, kKernelCount };
+enum KernelId {
+    kKSelect = 0, kKApply, kKEncode, kKScan, kKMoveEnd, kKHash,
+    // select latency telemetry (counters only, no launches): dependent tree levels walked
+    // (sum over trees of sum over descents of depth + 1), trees that descended, the current
+    // launch's slowest tree (folded into the sum by k_scan after every select), that sum
+    kKSelLevels, kKSelTrees, kKSelMax, kKSelMaxSum, kKernelCount
+};
 
 struct TreeCtl {
     int32_t sims_done;
@@ -458,14 +464,14 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 // simulations the reference spends re-finding the same queued leaf are
 // accounted by k.
 __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCache cache,
-                                                   unsigned long long *bytes_ctr) {
+                                                   unsigned long long *stats) {
     __shared__ float s_hit[kWavesPerBlock][kCacheVal];  // a cache hit's values, per wave
     const int lane = lane_id();
     const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (t >= tr.n_trees) return;
     TreeCtl ctl = tr.ctl[t];
     int pend = 0;
-    unsigned long long bytes = 0;
+    unsigned long long bytes = 0, levels = 0;
     if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
         const size_t base = (size_t)t * pool.cap;
         int32_t *__restrict__ N = pool.n + base;
@@ -556,6 +562,7 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
                 s = next_state(s, meta_action(lk.y));
             }
             if (fail) break;
+            levels += (unsigned long long)(depth + 1);
             const bool lose = is_lose(s);
             if (lose || legal_count(s) == 0u) {
                 // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
@@ -615,15 +622,24 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
     }
     if (lane == 0) {
         tr.pending[t] = pend;
-        if (bytes_ctr && bytes) atomicAdd(bytes_ctr, bytes);
+        if (stats && bytes) atomicAdd(stats + kKSelect, bytes);
+        if (stats && levels) {
+            atomicAdd(stats + kKSelLevels, levels);
+            atomicAdd(stats + kKSelTrees, 1ull);
+            atomicMax(stats + kKSelMax, levels);
+        }
     }
 }
 
 // ------------------------------------------------------------------- scan --
 // One block: exclusive scan of pending flags -> tree_of[slot] in tree order.
-__global__ __launch_bounds__(1024) void k_scan(Trees tr) {
+__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats) {
     __shared__ int sums[1024];
     const int tid = threadIdx.x;
+    if (stats && tid == 0) {  // the select launch before this scan is complete: fold its slowest tree
+        stats[kKSelMaxSum] += stats[kKSelMax];
+        stats[kKSelMax] = 0ull;
+    }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);
     int local = 0;
@@ -1438,13 +1454,13 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     {
         TimedLaunch tl(e, kKSelect);
         hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr, e->cache,
-                           bytes_ptr(e, kKSelect));
+                           e->timing ? e->d_bytes : nullptr);
     }
     int rc = check_launch();
     if (rc) return rc;
     {
         TimedLaunch tl(e, kKScan);
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr);
     }
     if ((rc = check_launch())) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));

@@ -719,6 +719,7 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
         case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;

@@ -16,7 +16,9 @@ UTTT_OK = 0
 ERRORS = {-1: "UTTT_ERR_ARG", -2: "UTTT_ERR_HIP", -3: "UTTT_ERR_CAPACITY", -4: "UTTT_ERR_ORDER",
           -5: "UTTT_ERR_NODEVICE"}
 
-KERNELS = {"select": 0, "apply": 1, "encode": 2, "scan": 3, "move_end": 4, "hash_eval": 5}
+KERNELS = {"select": 0, "apply": 1, "encode": 2, "scan": 3, "move_end": 4, "hash_eval": 5,
+           # select latency counters (their value is in "bytes"; no launches)
+           "select_levels": 6, "select_trees": 7, "select_max_levels_sum": 9}
 
 
 class UtttState(ctypes.Structure):

@@ -138,6 +138,9 @@ class FusedNetworkEvaluator:
         self.policy = torch.zeros((self.max_batch, 81), dtype=torch.float32, device=dev)
         self.value = torch.zeros((self.max_batch,), dtype=torch.float32, device=dev)
         self.states = None
+        # bench telemetry: when a list, every forward appends (n, start event, end event) recorded
+        # on its stream around the residual tower (2 x blocks conv launches)
+        self.tower_events = None
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -168,6 +171,9 @@ class FusedNetworkEvaluator:
     def _tower_heads(self, n, softmax):
         stream = self._stream()
         x, t, y = self.buf
+        if self.tower_events is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         if self.conv == "wino3h":
             fn = self.lib.uttt_nn_conv3x3_wino3h
             rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
@@ -188,6 +194,9 @@ class FusedNetworkEvaluator:
                 check(fn(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
                 check(fn(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
                 x, y = y, x
+        if self.tower_events is not None:
+            ev1.record()
+            self.tower_events.append((n, ev0, ev1))
         check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
                                      1 if softmax else 0, stream))
         return self.policy[:n], self.value[:n]
