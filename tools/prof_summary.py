@@ -29,7 +29,8 @@ def main(trace, bench_log, out):
                          int(r["VGPR_Count"]), int(r["SGPR_Count"]), int(r["Scratch_Size"])))
     rows.sort()
     sel = [r for r in rows if "k_select" in r[2]]
-    nwin = bench["roofline"]["launches"]
+    rs = bench.get("roofline_select", bench["roofline"])
+    nwin = rs["launches"]
     t0 = sel[-nwin][0] if len(sel) >= nwin else rows[0][0]
     win = [r for r in rows if r[0] >= t0]
     agg = defaultdict(lambda: [0, 0, 0, 0, 0])
@@ -47,12 +48,22 @@ def main(trace, bench_log, out):
     for n, a in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
         lines.append(f"| `{n}` | {a[0]} | {a[1] / 1e6:.2f} | {100 * a[1] / total:.2f} | {a[1] / a[0] / 1e3:.1f} | "
                      f"{a[2]} | {a[3]} | {a[4]} |")
-    sw = [r for r in win if "k_select" in r[2]]
-    avg_sel = sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3
-    lines += ["", f"k_select in window: {len(sw)} dispatches, avg {avg_sel:.1f} us (rocprof) vs "
-                  f"{bench['roofline']['avg_launch_us']} us (bench HIP events); "
-                  f"algorithmic bytes/launch {bench['roofline']['algo_bytes_per_launch']} -> "
-                  f"{bench['roofline']['algo_bytes_per_launch'] / (avg_sel * 1e3):.2f} GB/s (rocprof time)"]
+    lines.append("")
+    for key in ("roofline", "roofline_select", "roofline_backup"):
+        rf = bench.get(key)
+        if not rf:
+            continue
+        kname = rf["kernel"].split()[0]
+        sw = [r for r in win if kname in r[2]]
+        avg = sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3
+        if rf["unit"] == "TFLOP/s":
+            work = rf["executed_flop_per_board"] * rf["boards_per_launch"]
+            rate = f"{work / (avg * 1e-6) / 1e12:.1f} TFLOP/s executed MFMA flops (rocprof time)"
+        else:
+            work = rf["algo_bytes_per_launch"]
+            rate = f"{work / (avg * 1e3):.2f} GB/s algorithmic (rocprof time)"
+        lines.append(f"- `{kname}` in window: {len(sw)} dispatches, avg {avg:.1f} us (rocprof) vs "
+                     f"{rf['avg_launch_us']} us (bench HIP events, {rf['launches']} launches) -> {rate}")
     with open(out, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
