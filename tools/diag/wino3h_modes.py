@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Time k_wino3h_conv variants (uttt_diag_wino3h_ablation MODEs) against the product
+launch at the given board counts and check that product variants give the product's
+output bits. usage: MODES=0,1024 wino3h_modes.py 1344 16384"""
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(REPO, "ultimate-tictactoe-alphazero_amd")]
+
+import torch  # noqa: E402
+from uttt_amd import _lib  # noqa: E402
+from uttt_amd.model import fold_bn, random_network  # noqa: E402
+from uttt_amd.nnfast import board_amax, wino3h_weights, _p  # noqa: E402
+
+# diagnostic-only MODE bits that change the output (no transform / GEMM / fold / stores)
+LOSSY = 1 | 2 | 8 | 16 | 32 | 64
+
+
+def timeit(fn, reps=30):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps
+
+
+def main():
+    lib = _lib.load()
+    lib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+    net = random_network(0)
+    w, b = fold_bn(net.residual_blocks[8].conv1, net.residual_blocks[8].bn1)
+    uh, su = wino3h_weights(w)
+    uh, b = uh.cuda(), b.cuda()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    modes = [int(v) for v in os.environ.get("MODES", "0,1024").split(",")]
+    u8 = uh.repeat(8)  # 8 replicas for the placement diagnostics (MODE 256 / 8192)
+    for n in [int(a) for a in (sys.argv[1:] or ["1344", "16384"])]:
+        g = torch.Generator(device="cuda").manual_seed(n)
+        x = torch.relu(torch.randn(n, 81, 128, device="cuda", generator=g))
+        ba = board_amax(x)
+        y0 = torch.empty_like(x)
+        t_prod = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y0),
+                                                          _p(ba), 1, None, None, 0, n, st))
+        rec = {"boards": n, "product_us": round(t_prod, 1), "modes": {}}
+        for m in modes:
+            y = torch.full_like(x, float("nan"))
+            # the ablation launch takes one max for every board: pass the product's per-board row
+            # through a per-board launch is not available there, so use a uniform bound
+            t = timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(u8 if m & (256 | 8192) else uh),
+                                                                  ctypes.c_float(su), _p(b), _p(y),
+                                                                  _p(ba.max().reshape(1)), n, m, st))
+            ent = {"us": round(t, 1), "tflops_exec": round(22118400 * n / t / 1e6, 1)}
+            if not (m & LOSSY):
+                if m == modes[0]:
+                    yref = y.clone()
+                ent["bits_equal_first_mode"] = bool(torch.equal(y, yref))
+                if not ent["bits_equal_first_mode"]:
+                    d = (y - yref).abs()
+                    ent["n_diff"] = int((d > 0).sum().item())
+                    ent["max_rel_diff"] = (d.max() / yref.abs().max()).item()
+            rec["modes"][str(m)] = ent
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
