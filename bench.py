@@ -32,14 +32,12 @@ PKG = os.path.join(REPO, "ultimate-tictactoe-alphazero_amd")
 METRIC = "MCTS simulations/sec (whole node), 4096 games × 50 sims/move; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense
-FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 MFMA (= vector) peak
 NETCAL = os.path.join(REPO, "tests", "golden", "netcal.npz")
 
 # residual-tower conv, per board: MFMA flops the kernels issue, and the direct 3x3 conv's flops
-CONV_EXEC_FLOP = {"wino3h": 3 * 9 * 25 * 128 * 128 * 2,   # F(3x3,3x3): 9 tiles x 25 points, 3 f16 products
-                  "wino3": 9 * 25 * 128 * 128 * 2}        # the same on the f32 MFMA, 1 product
+CONV_EXEC_FLOP = {"wino3h": 3 * 9 * 25 * 128 * 128 * 2}  # F(3x3,3x3): 9 tiles x 25 points, 3 f16 products
 CONV_DIRECT_FLOP = 2 * 81 * 128 * 1152
-CONV_PEAK = {"wino3h": F16_DENSE_PEAK_TFLOPS, "wino3": FP32_PEAK_TFLOPS}
+CONV_PEAK = {"wino3h": F16_DENSE_PEAK_TFLOPS}
 # residual-tower conv, algorithmic HBM bytes per board: read x, write y (+ read the residual on
 # every second conv); the transformed weights (1.6 MB) are read once per launch, L2/MALL-resident
 CONV_BYTES_PER_BOARD = 81 * 128 * 4 * 2.5
@@ -63,7 +61,7 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "fused-f32", "nn", "hash"], default="fused")
+    ap.add_argument("--evaluator", choices=["fused", "nn", "hash"], default="fused")
     ap.add_argument("--net", choices=["seed0", "calibrated"], default="seed0",
                     help="seed0: the reference's initial best.pth; calibrated: tests/golden/netcal.npz")
     ap.add_argument("--age", type=int, default=100,
@@ -208,7 +206,7 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
 
     dev = torch.device("cuda", local)
     sp = SelfPlay(games, sims, batch, 1.0, device=local, cache_log2=cache_log2, lanes=lanes)
-    conv = {"fused": "wino3h", "fused-f32": "wino3"}.get(evaluator)
+    conv = {"fused": "wino3h"}.get(evaluator)
     tower_events = []
     if evaluator == "hash":
         make_inner = HashEvaluator
@@ -413,7 +411,7 @@ def main():
             "vs_baseline": None,
             "dtype": {"fused": "f32 activations and accumulation; tower point GEMMs as 3-term split-f16 products "
                                "on the f16 MFMA (f32-level accuracy: within 1e-5 of the reference's fp32 network)",
-                      "fused-f32": "f32", "nn": "f32", "hash": "f32 (hash evaluator)"}[args.evaluator],
+                      "nn": "f32", "hash": "f32 (hash evaluator)"}[args.evaluator],
             "data": "synthetic: self-play from the initial position, games refilled as they end; DualNetwork "
                     + ("random init torch.manual_seed(0) (the reference's initial best.pth)" if args.net == "seed0"
                        else "with calibrated BatchNorm statistics (tests/golden/netcal.npz)") + "; no checkpoint",
@@ -426,8 +424,6 @@ def main():
                 "evaluator": {"fused": "DualNetwork 128f x16 on HIP kernels: stem from bitboards, residual tower as "
                                        "fused Winograd F(3x3,3x3) convs (csrc/wino3h_conv.hip, split-f16 MFMA, f32 "
                                        "accumulation, per-board scaling), heads (csrc/nn_kernels.hip)",
-                              "fused-f32": "DualNetwork 128f x16 on HIP kernels, tower on the f32 MFMA "
-                                           "(csrc/wino3_conv.hip)",
                               "nn": "DualNetwork 128f x16 fp32, BN folded, PyTorch-ROCm/MIOpen",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],
                 "parallelism": f"games sharded over {world} GPU(s) by contiguous global-id blocks, "

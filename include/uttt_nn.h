@@ -47,26 +47,20 @@ int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float 
                   int32_t softmax, void *stream);
 
 /* Residual-tower 3x3 conv (128->128, pad 1, 9x9 boards) + bias (+ residual) + ReLU as one
- * Winograd F(3x3,3x3) f32-MFMA kernel (csrc/wino3_conv.hip): a 9x9 board is exactly 3x3 tiles
- * of 3x3 outputs, 25 transform points (Toom-Cook on {0,1,-1,2,inf}). x, residual, y:
- * [n_boards][81][128] NHWC; y must not alias x or residual. u: 25*128*128 floats,
- * U[xi][ci][co] = G g G^T from uttt_nn_wino3_weights (host, double) of a folded conv weight
- * w[128 co][128 ci][3][3], stored as U[xi][ci/16][co][ci%4][(ci%16)/4]. */
-int uttt_nn_wino3_weights(const float *w, float *u);
-int uttt_nn_conv3x3_wino3(const float *x, const float *u, const float *bias, const float *residual, float *y,
-                          int32_t n_boards, void *stream);
-
-/* The same F(3x3,3x3) conv with its point GEMMs on the f16 matrix cores at f32-level accuracy
- * (csrc/wino3h_conv.hip): V and U are each split into f16 hi + lo halves (power-of-two scaled into
- * f16 range) and M = Vhi Uhi + Vhi Ulo + Vlo Uhi accumulates in f32.
- * uttt_nn_wino3h_weights: u receives 25*128*128*2 f16 (hi, lo) in the kernel's B-fragment order
- * U[xi][ci/32][hi|lo][co][(ci%32)/8][ci%8], *u_scale the power of two U was scaled by.
+ * Winograd F(3x3,3x3) kernel (csrc/wino3h_conv.hip; dual_network.py:28-45): a 9x9 board is
+ * exactly 3x3 tiles of 3x3 outputs, 25 transform points (Toom-Cook on {0,1,-1,2,inf}). The point
+ * GEMMs run on the f16 matrix cores at f32-level accuracy: V and U are each split into f16
+ * hi + lo halves (power-of-two scaled into f16 range) and M = Vhi Uhi + Vhi Ulo + Vlo Uhi
+ * accumulates in f32. x, residual, y: [n_boards][81][128] NHWC; y must not alias x or residual.
+ * uttt_nn_wino3h_weights: U = G g G^T (host, double) of a folded conv weight w[128 co][128 ci][3][3];
+ * u receives 25*128*128*2 f16 (hi, lo) in the kernel's A-fragment order
+ * U[xi][ci/32][hi|lo][co/16][(ci%32)/8][co%16][ci%8], *u_scale the power of two U was scaled by.
  * uttt_nn_conv3x3_wino3h: V is scaled per board, so a board's outputs depend on its own inputs only.
  * x_amax (required): max|x| as u32 float bits, one per board when x_amax_per_board != 0 (e.g. the
  * y_amax row of the conv that produced x), else one bound x_amax[0] for every board (the stem).
  * y_amax (optional): receives max(y) of each board by atomic max (the row must be zero on entry).
  * amax_clear (optional): the kernel zeroes amax_clear[0 .. clear_count), for a later conv's y_amax;
- * it must not be x_amax or y_amax. Other rules as uttt_nn_conv3x3_wino3. */
+ * it must not be x_amax or y_amax. */
 int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale);
 int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias,
                            const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,

@@ -298,8 +298,7 @@ def test_fused_evaluator_matches_cpu_fp32(gpu, oracle_lib):
     bs = gpu.BatchedSearch(len(roots), 50)
     for make, sat in ((lambda d: random_network(0, d), True), (lambda d: calibrated_network(NETCAL, d), False)):
         net = make("cuda")
-        for conv in ("wino3h", "wino3"):
-            _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine, conv=conv), make("cpu"), sat)
+        _fused_vs_cpu(gpu, bs, roots, FusedNetworkEvaluator(net, bs.engine), make("cpu"), sat)
 
 
 def _fused_vs_cpu(gpu, bs, roots, fused, cpu, saturated):
@@ -393,31 +392,6 @@ def test_eval_cache_is_exact(gpu, oracle_lib):
     assert st["hits"] > 0 and st["inserts"] > 0
 
 
-def test_winograd_conv_matches_torch_fp32(gpu):
-    """The f32-MFMA F(3x3,3x3) conv (+bias, +residual, ReLU) vs an f64 conv2d on the same
-    folded weights, for ragged board counts (tail workgroups)."""
-    import torch
-    import torch.nn.functional as F
-    from uttt_amd.model import fold_bn, random_network
-    from uttt_amd.nnfast import conv3x3_wino3, wino3_weights
-    net = random_network(3)
-    blk = net.residual_blocks[5]
-    w, b = fold_bn(blk.conv1, blk.bn1)
-    u = wino3_weights(w).cuda()
-    w, b = w.cuda(), b.cuda()
-    g = torch.Generator().manual_seed(1)
-    for n in (1, 3, 4, 5, 64, 257, 1000):
-        x = torch.randn(n, 81, 128, generator=g).cuda()
-        r = torch.randn(n, 81, 128, generator=g).cuda()
-        xn = x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2)
-        ref = F.conv2d(xn.double(), w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
-        for res in (None, r):
-            y = conv3x3_wino3(x, u, b, res)
-            want = torch.relu(ref + (res.double() if res is not None else 0)).float()
-            err = (y - want).abs().max().item()
-            assert err <= 1e-5 * max(1.0, want.abs().max().item()), (n, res is None, err)
-
-
 def test_split_f16_winograd_conv_matches_f64(gpu):
     """The split-f16 F(3x3,3x3) kernel (wino3h) vs an f64 direct conv: within 1e-5 of each
     board's output scale (the bar the f32 kernels meet) for ragged board counts (partial last
@@ -489,7 +463,7 @@ def test_networks_match_reference_on_calibrated_net(gpu):
     torch.backends.cuda.matmul.allow_tf32 = False
     net = calibrated_network(NETCAL, "cuda")
     outs = {}
-    for conv in ("wino3h", "wino3"):
+    for conv in ("wino3h",):
         fe = FusedNetworkEvaluator(net, None, max_batch=len(states), conv=conv)
         p, v = fe.forward_states(states)
         outs["fused-" + conv] = (p.cpu().numpy(), v.cpu().numpy())
@@ -518,7 +492,7 @@ def test_fused_outputs_do_not_depend_on_the_batch(gpu):
     rng = np.random.RandomState(9)
     others = _rules_states(rng.choice(np.nonzero(r["n_legal"] > 0)[0], 1000, replace=False))
     net = calibrated_network(NETCAL, "cuda")
-    for conv in ("wino3h", "wino3"):
+    for conv in ("wino3h",):
         fe = FusedNetworkEvaluator(net, None, max_batch=1100, conv=conv)
         p0, v0 = (t.clone() for t in fe.forward_states(mine))
         big = np.concatenate([others[:37], mine, others[37:]])

@@ -136,17 +136,24 @@ def test_calibrated_network_reproduces_reference_fixture():
 
 
 def test_winograd3_algebra_matches_direct_conv(engine_lib):
-    """Winograd F(3x3,3x3) as k_wino3_conv computes it (U from uttt_nn_wino3_weights;
-    V = B^T d B on the 5x5 windows of the zero-padded board; Y = A^T (U . V) A on
-    3x3 tiles of 3x3 outputs, nothing cropped) equals the direct 3x3 conv."""
+    """Winograd F(3x3,3x3) as k_wino3h_conv computes it (U from uttt_nn_wino3h_weights, the
+    f16 hi + lo halves recombined and unscaled; V = B^T d B on the 5x5 windows of the
+    zero-padded board; Y = A^T (U . V) A on 3x3 tiles of 3x3 outputs, nothing cropped) equals
+    the direct 3x3 conv."""
     import ctypes
     rng = np.random.RandomState(1)
     w = rng.randn(128, 128, 3, 3).astype(np.float32)
-    u = np.zeros((25, 128, 128), np.float32)
+    uh = np.zeros(25 * 128 * 128 * 2, np.uint16)
+    su = ctypes.c_float(0.0)
     fp = ctypes.POINTER(ctypes.c_float)
-    assert engine_lib.uttt_nn_wino3_weights(w.ctypes.data_as(fp), u.ctypes.data_as(fp)) == 0
-    # stored order U[xi][ci/16][co][ci%4][(ci%16)/4] -> U[xi][ci][co]
-    u = u.reshape(25, 8, 128, 4, 4).transpose(0, 1, 4, 3, 2).reshape(25, 128, 128)
+    assert engine_lib.uttt_nn_wino3h_weights(w.ctypes.data_as(fp), ctypes.c_void_p(uh.ctypes.data),
+                                             ctypes.byref(su)) == 0
+    assert su.value > 0 and np.log2(su.value) == int(np.log2(su.value))
+    # stored order U[xi][ci/32][hi|lo][co/16][(ci%32)/8][co%16][ci%8] -> (hi, lo)[xi][ci][co]
+    h = uh.view(np.float16).astype(np.float64).reshape(25, 4, 2, 8, 4, 16, 8)
+    h = h.transpose(2, 0, 1, 4, 6, 3, 5).reshape(2, 25, 128, 128)
+    u = (h[0] + h[1]) / su.value
+    assert np.abs(h[1]).max() <= np.abs(h[0]).max() * 2.0 ** -10  # lo is the rounding remainder of hi
     BT = np.array([[2, -1, -2, 1, 0], [0, -2, -1, 1, 0], [0, 2, -3, 1, 0], [0, -1, 0, 1, 0], [0, 2, -1, -2, 1]],
                   np.float64)
     AT = np.array([[1, 1, 1, 1, 0], [0, 1, -1, 2, 0], [0, 1, 1, 4, 1]], np.float64)

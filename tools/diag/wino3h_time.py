@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Time the conv kernels at bench-like and large batches: MIOpen-free comparison of
-k_wino3_conv (f32 MFMA) and k_wino3h_conv (split-f16 MFMA), plus wino3h ablations
-(1 no transform, 2 no point GEMMs, 64 no fold). Accuracy vs f64 printed alongside."""
+"""Time k_wino3h_conv (split-f16 MFMA) at bench-like and large batches, plus its ablations
+(1 no transform, 2 no point GEMMs, 64 no fold, ...) and prefetch-distance variants.
+Accuracy vs f64 printed alongside."""
 import ctypes
 import json
 import os
@@ -14,7 +14,7 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 from uttt_amd import _lib  # noqa: E402
 from uttt_amd.model import fold_bn, random_network  # noqa: E402
-from uttt_amd.nnfast import amax, board_amax, conv3x3_wino3h, wino3_weights, wino3h_weights, _p  # noqa: E402
+from uttt_amd.nnfast import amax, board_amax, conv3x3_wino3h, wino3h_weights, _p  # noqa: E402
 
 
 def timeit(fn, reps=20):
@@ -35,7 +35,6 @@ def main():
         [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
     net = random_network(0)
     w, b = fold_bn(net.residual_blocks[8].conv1, net.residual_blocks[8].bn1)
-    u3 = wino3_weights(w).cuda()
     uh, su = wino3h_weights(w)
     uh, b, wc = uh.cuda(), b.cuda(), w.cuda()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -44,7 +43,6 @@ def main():
         x = torch.relu(torch.randn(n, 81, 128, device="cuda"))
         y = torch.empty_like(x)
         xa = amax(x)
-        t3 = timeit(lambda: lib.uttt_nn_conv3x3_wino3(_p(x), _p(u3), _p(b), None, _p(y), n, st))
         ba = board_amax(x)
         th = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y), _p(ba), 1,
                                                       None, None, 0, n, st))
@@ -61,18 +59,14 @@ def main():
         ref = F.conv2d(xs.reshape(-1, 9, 9, 128).permute(0, 3, 1, 2).double(), wc.double(), b.double(), padding=1)
         ref = torch.relu(ref).permute(0, 2, 3, 1).reshape(-1, 81, 128)
         yh = conv3x3_wino3h(xs, uh, su, b)
-        y3 = torch.empty_like(xs)
-        lib.uttt_nn_conv3x3_wino3(_p(xs), _p(u3), _p(b), None, _p(y3), xs.shape[0], st)
         torch.cuda.synchronize()
         sc = ref.abs().max().item()
         u8 = uh.repeat(8)
         abl[256] = timeit(lambda: lib.uttt_diag_wino3h_ablation(_p(x), _p(u8), ctypes.c_float(su), _p(b), _p(y),
                                                                 _p(xa), n, 256, st))
-        rec = {"boards": n, "wino3_f32_us": round(t3, 1), "wino3h_us": round(th, 1), "wino3h_res_us": round(th_res, 1),
-               "speedup": round(t3 / th, 2), "ablation_us": {str(k): round(v, 1) for k, v in abl.items()},
+        rec = {"boards": n, "wino3h_us": round(th, 1), "wino3h_res_us": round(th_res, 1), "ablation_us": {str(k): round(v, 1) for k, v in abl.items()},
                "direct_equiv_tflops": round(2 * 81 * 128 * 1152 * n / th / 1e6, 1),
-               "err_rel_wino3h": (yh.double() - ref).abs().max().item() / sc,
-               "err_rel_wino3": (y3.double() - ref).abs().max().item() / sc}
+               "err_rel_wino3h": (yh.double() - ref).abs().max().item() / sc}
         print(json.dumps(rec), flush=True)
         out.append(rec)
 

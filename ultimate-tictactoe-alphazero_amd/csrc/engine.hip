@@ -36,16 +36,7 @@
 namespace uttt {
 
 // ------------------------------------------------------------------ errors --
-static thread_local std::string g_err;
-
-void set_error(const char *fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    g_err = buf;
-}
+void set_error(const char *fmt, ...);  // rules_api.cpp (uttt_last_error)
 
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
@@ -863,10 +854,10 @@ __global__ void k_root_visits(Pool pool, Trees tr, int32_t *visits, int32_t *n_l
 __global__ void k_root_scores(Pool pool, Trees tr, float temperature, float *scores, int32_t *n_legal) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= tr.n_trees) return;
-    float sc[81];
+    float *sc = scores + (size_t)t * 81;  // the output row is the working buffer (no scratch)
     int L;
     root_scores(pool, (size_t)t * pool.cap, temperature, sc, L);
-    for (int i = 0; i < 81; ++i) scores[(size_t)t * 81 + i] = i < L ? sc[i] : 0.0f;
+    for (int i = L; i < 81; ++i) sc[i] = 0.0f;
     n_legal[t] = L;
 }
 
@@ -962,7 +953,9 @@ __device__ double np_sum(const double *a, int n) {
     return res;  // n <= 81 < 128: a single pairwise block
 }
 
-// One thread per slot: the per-move tail of self_play_cpp.play (:63-92).
+// One thread per slot: the per-move tail of self_play_cpp.play (:63-92). The slot's
+// f64 policy-target row of this ply (81 doubles in HBM) is the working buffer: no
+// per-thread arrays, so nothing lives in scratch.
 __global__ void k_move_end(Pool pool, SelfPlay sp) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= sp.slots) return;
@@ -973,43 +966,71 @@ __global__ void k_move_end(Pool pool, SelfPlay sp) {
         return;
     }
     const size_t base = (size_t)s * pool.cap;
-    float sc[81];
-    int L;
-    root_scores(pool, base, sp.temperature, sc, L);
-    // scores -> float64, renormalised with np.sum (:74-78)
-    double d[81];
-    for (int i = 0; i < L; ++i) d[i] = (double)sc[i];
-    const double tot = np_sum(d, L);
-    if (tot == 0.0) {
-        for (int i = 0; i < L; ++i) d[i] = 1.0 / (double)L;
-    } else {
-        for (int i = 0; i < L; ++i) d[i] = d[i] / tot;
-    }
-    // legal actions (ascending) of the root
-    uint32_t m[3];
-    legal_mask(sl.state, m);
-    int8_t leg[81];
-    int nl = 0;
-    for (int w = 0; w < 3; ++w)
-        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) leg[nl++] = (int8_t)(27 * w + __builtin_ctz(bits));
-    // policy target (:81-83) into the slot's ply buffer
     const int ply = sl.ply;
     double *pt = sp.ply_policy + ((size_t)s * kMaxPlies + ply) * 81;
-    for (int a = 0; a < 81; ++a) pt[a] = 0.0;
-    for (int i = 0; i < L; ++i) pt[leg[i]] = d[i];
-    // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right
-    double acc = 0.0;
-    for (int i = 0; i < L; ++i) {
-        acc += d[i];
-        d[i] = acc;
+    // root scores (uttt_mcts.cpp:177-192, as root_scores) as f32 values held exactly in pt[0..L)
+    int first;
+    const int L = root_children(pool, base, first);
+    if (sp.temperature == 0.0f) {
+        int mi = 0;
+        float mv = L ? (float)pool.n[base + first] : 0.0f;
+        for (int i = 1; i < L; ++i) {
+            const float v = (float)pool.n[base + first + i];
+            if (v > mv) {
+                mv = v;
+                mi = i;
+            }
+        }
+        for (int i = 0; i < L; ++i) pt[i] = (i == mi) ? 1.0 : 0.0;
+    } else {
+        const double y = (double)(1.0f / sp.temperature);  // glibc powf: double pow, one rounding
+        float sum = 0.0f;
+        for (int i = 0; i < L; ++i) {
+            const float v = (float)pow((double)pool.n[base + first + i], y);
+            pt[i] = (double)v;
+            sum += v;
+        }
+        if (sum > 0)
+            for (int i = 0; i < L; ++i) pt[i] = (double)((float)pt[i] / sum);
     }
-    const double last = d[L - 1];
+    // scores -> float64, renormalised with np.sum (:74-78)
+    const double tot = np_sum(pt, L);
+    for (int i = 0; i < L; ++i) pt[i] = (tot == 0.0) ? 1.0 / (double)L : pt[i] / tot;
+    // policy target (:81-83): entry i moves to its action (the i-th legal action >= i, so a
+    // descending scatter never overwrites an entry it still has to move), the rest are zero
+    uint32_t m[3];
+    legal_mask(sl.state, m);
+    {
+        int i = L - 1;
+        for (int w = 2; w >= 0; --w)
+            for (int b = 26; b >= 0; --b)
+                if ((m[w] >> b) & 1u) {
+                    pt[27 * w + b] = pt[i];
+                    --i;
+                }
+        for (int a = 0; a < 81; ++a)
+            if (!((m[a / 27] >> (a % 27)) & 1u)) pt[a] = 0.0;
+    }
+    // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right.
+    // Two passes over the legal actions in order, the same additions in the same order.
+    double last = 0.0;
+    for (int w = 0; w < 3; ++w)
+        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) last += pt[27 * w + __builtin_ctz(bits)];
     uint32_t *key = sp.mt_key + (size_t)s * 624;
     const double u = mt_double(key, sp.mt_pos + s);
-    int idx = 0;
-    while (idx < L && d[idx] / last <= u) ++idx;
-    if (idx >= L) idx = L - 1;
-    const int action = leg[idx];
+    int action = -1, final_action = -1;
+    double acc = 0.0;
+    for (int w = 0; w < 3 && action < 0; ++w)
+        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) {
+            const int a = 27 * w + __builtin_ctz(bits);
+            acc += pt[a];
+            final_action = a;
+            if (!(acc / last <= u)) {
+                action = a;
+                break;
+            }
+        }
+    if (action < 0) action = final_action;  // idx >= L -> L - 1
     sp.ply_state[(size_t)s * kMaxPlies + ply] = sl.state;
     sp.ply_action[(size_t)s * kMaxPlies + ply] = (int8_t)action;
     sl.state = next_state(sl.state, action);
@@ -1300,7 +1321,6 @@ int engine_pending_view(uttt_engine_t *e, const uttt_state_t **leaf, const int32
 
 extern "C" {
 
-const char *uttt_last_error(void) { return g_err.c_str(); }
 const char *uttt_version(void) { return "uttt-mi355x 0.1 (gfx950)"; }
 
 int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out) {

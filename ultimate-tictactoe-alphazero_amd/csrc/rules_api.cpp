@@ -2,6 +2,7 @@
 // type behind `uttt_cpp.State` (cpp/python_bindings.cpp:53-74). Same bitboard
 // code the kernels use (uttt_bits.h).
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -10,12 +11,25 @@
 #include "uttt_engine.h"
 
 namespace uttt {
-void set_error(const char *fmt, ...);
+// Last error of the calling thread, for every entry point of the C ABI (uttt_last_error).
+// Kept in this host-only file so the rules build on their own (tests/asan).
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
 }
+}  // namespace uttt
 
 using namespace uttt;
 
 extern "C" {
+
+const char *uttt_last_error(void) { return g_err.c_str(); }
 
 void uttt_state_initial(uttt_state_t *out) {
     std::memset(out, 0, sizeof(*out));

@@ -90,8 +90,6 @@ SIGNATURES = {
     "uttt_nn_stem": (ctypes.c_int, [_P, _P, _P, _P]),
     "uttt_nn_stem_states": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P]),
     "uttt_nn_heads": (ctypes.c_int, [_P, _P, _I32, _P, _P, _I32, _P]),
-    "uttt_nn_wino3_weights": (ctypes.c_int, [_F32P, _F32P]),
-    "uttt_nn_conv3x3_wino3": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _P]),
     "uttt_nn_wino3h_weights": (ctypes.c_int, [_F32P, _P, ctypes.POINTER(ctypes.c_float)]),
     "uttt_nn_conv3x3_wino3h": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, _P, _P, _P, _I32, _P, _P, _I32, _I32, _P]),
     "uttt_nn_amax": (ctypes.c_int, [_P, _I64, _P, _P]),

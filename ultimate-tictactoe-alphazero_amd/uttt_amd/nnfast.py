@@ -1,10 +1,9 @@
 """FusedNetworkEvaluator: the DualNetwork leaf evaluator as gfx950 kernels
-(csrc/nn_kernels.hip, csrc/wino3h_conv.hip, csrc/wino3_conv.hip, include/uttt_nn.h):
+(csrc/nn_kernels.hip, csrc/wino3h_conv.hip, include/uttt_nn.h):
 
   leaves --k_stem--> act (n,81,128 NHWC, relu(conv_input+bn) applied, straight from bitboards)
-  16 x [ conv3x3 + b1 + ReLU            (conv="wino3h", default: Winograd F(3x3,3x3), split-f16
-         conv3x3 + b2 + residual + ReLU ]  MFMA, f32 accumulation; conv="wino3": the same on the
-                                           f32 MFMA)
+  16 x [ conv3x3 + b1 + ReLU            (Winograd F(3x3,3x3), point GEMMs as split-f16 products
+         conv3x3 + b2 + residual + ReLU ]  on the f16 MFMA, f32 accumulation)
   --k_heads--> policy (n,81) softmax, value (n,)
 
 BatchNorm is folded (eval mode), so the function is the reference's
@@ -85,11 +84,8 @@ def _prepared_weights(net, dev, conv):
         pair = []
         for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
             w, bb = fold_bn(cv, bn)
-            if conv == "wino3h":
-                u, su = wino3h_weights(w)
-                pair.append((u.to(dev), su, bb.to(dev)))
-            else:
-                pair.append((wino3_weights(w).to(dev), None, bb.to(dev)))
+            u, su = wino3h_weights(w)
+            pair.append((u.to(dev), su, bb.to(dev)))
         out["wino"].append(tuple(pair))
     # the stem's output bound for every board: relu(b + sum of the positive weight rows), inputs 0/1
     out["stem_bound"] = float(torch.relu(out["stem_b"].double().cpu() +
@@ -106,8 +102,8 @@ class FusedNetworkEvaluator:
 
     def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None):
         net = net.eval()
-        if conv not in ("wino3h", "wino3"):
-            raise ValueError("conv must be 'wino3h' or 'wino3'")
+        if conv != "wino3h":
+            raise ValueError("conv must be 'wino3h' (the split-f16 Winograd tower; the f32-MFMA kernel was retired)")
         self.conv = conv
         self.engine = engine
         self.lib = _lib.load()
@@ -126,15 +122,14 @@ class FusedNetworkEvaluator:
         w = _prepared_weights(net, dev, conv)
         self.stem_w, self.stem_b, self.heads, self.wino = w["stem_w"], w["stem_b"], w["heads"], w["wino"]
         self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
-        if conv == "wino3h":
-            # The stem's output is bounded for every board by relu(b + sum of the positive weight
-            # rows) (its inputs are 0/1 planes): one scale for all boards. Conv i then reads the
-            # per-board maxima of its input from row (i-1) % 4, atomically maxes its own output
-            # into row i % 4 and zeroes row (i+1) % 4 for conv i+1; 32 convs per forward keep
-            # the rotation aligned across forwards, so no fill kernel is ever needed.
-            self.stem_bound = w["stem_bound"]
-            self.stem_amax = torch.tensor([self.stem_bound], dtype=torch.float32, device=dev).view(torch.int32)
-            self.bamax = torch.zeros((self.NROW, self.max_batch), dtype=torch.int32, device=dev)
+        # The stem's output is bounded for every board by relu(b + sum of the positive weight
+        # rows) (its inputs are 0/1 planes): one scale for all boards. Conv i then reads the
+        # per-board maxima of its input from row (i-1) % 4, atomically maxes its own output
+        # into row i % 4 and zeroes row (i+1) % 4 for conv i+1; 32 convs per forward keep
+        # the rotation aligned across forwards, so no fill kernel is ever needed.
+        self.stem_bound = w["stem_bound"]
+        self.stem_amax = torch.tensor([self.stem_bound], dtype=torch.float32, device=dev).view(torch.int32)
+        self.bamax = torch.zeros((self.NROW, self.max_batch), dtype=torch.int32, device=dev)
         self.policy = torch.zeros((self.max_batch, 81), dtype=torch.float32, device=dev)
         self.value = torch.zeros((self.max_batch,), dtype=torch.float32, device=dev)
         self.states = None
@@ -174,26 +169,19 @@ class FusedNetworkEvaluator:
         if self.tower_events is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        if self.conv == "wino3h":
-            fn = self.lib.uttt_nn_conv3x3_wino3h
-            rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
-            cap = self.max_batch
-            i = 0
-            for (u1, s1, b1), (u2, s2, b2) in self.wino:
-                src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
-                check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), src[0], src[1], rows[i % 4],
-                         rows[(i + 1) % 4], cap, n, stream))
-                i += 1
-                check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), rows[(i - 1) % 4], 1, rows[i % 4],
-                         rows[(i + 1) % 4], cap, n, stream))
-                i += 1
-                x, y = y, x
-        else:
-            fn = self.lib.uttt_nn_conv3x3_wino3
-            for (u1, _, b1), (u2, _, b2) in self.wino:
-                check(fn(_p(x), _p(u1), _p(b1), None, _p(t), n, stream))
-                check(fn(_p(t), _p(u2), _p(b2), _p(x), _p(y), n, stream))
-                x, y = y, x
+        fn = self.lib.uttt_nn_conv3x3_wino3h
+        rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
+        cap = self.max_batch
+        i = 0
+        for (u1, s1, b1), (u2, s2, b2) in self.wino:
+            src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
+            check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), src[0], src[1], rows[i % 4],
+                     rows[(i + 1) % 4], cap, n, stream))
+            i += 1
+            check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), rows[(i - 1) % 4], 1, rows[i % 4],
+                     rows[(i + 1) % 4], cap, n, stream))
+            i += 1
+            x, y = y, x
         if self.tower_events is not None:
             ev1.record()
             self.tower_events.append((n, ev0, ev1))
@@ -203,17 +191,6 @@ class FusedNetworkEvaluator:
 
     def __call__(self, x, n):
         return self.forward(n, True)
-
-
-def wino3_weights(w):
-    """Folded conv weight (128,128,3,3) -> Winograd F(3x3,3x3) U, 25*128*128 floats in kernel order (host, double)."""
-    import numpy as np
-    wc = np.ascontiguousarray(w.detach().float().cpu().numpy())
-    u = np.zeros((25, 128, 128), np.float32)
-    lib = _lib.load()
-    check(lib.uttt_nn_wino3_weights(wc.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-                                    u.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
-    return torch.from_numpy(u)
 
 
 def wino3h_weights(w):
@@ -252,15 +229,6 @@ def conv3x3_wino3h(x, u, su, bias, residual=None, y_amax=None, x_amax=None):
                                              _p(residual) if residual is not None else None, _p(y), _p(xa), 1,
                                              _p(y_amax) if y_amax is not None else None, None, 0, x.shape[0],
                                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
-    return y
-
-
-def conv3x3_wino3(x, u, bias, residual=None):
-    """Test/utility wrapper: x (n,81,128) f32 cuda -> relu(conv3x3(x) + bias (+ residual)), u from
-    wino3_weights() (the f32-MFMA F(3x3,3x3) kernel)."""
-    y = torch.empty_like(x)
-    check(_lib.load().uttt_nn_conv3x3_wino3(_p(x), _p(u), _p(bias), _p(residual) if residual is not None else None,
-                                            _p(y), x.shape[0], ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return y
 
 
