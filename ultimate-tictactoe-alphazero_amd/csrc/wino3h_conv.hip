@@ -106,6 +106,11 @@ __device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], flo
     constexpr int u = P / 5, v = P % 5;
     if constexpr (O < 4 * n_rows(u)) {
         constexpr int a = nth_row(u, O / 4), j = O % 4, K = at(a, u);
+        // Inline asm is outside the compiler's hazard recognizer, so nothing pads these reads of
+        // the previous point's MFMA results; the schedule keeps >= 6 instructions, one of them an
+        // MFMA, between producer and reader, and the output bits equal those of a compiler-visible
+        // fold (builtin packed ops, hazard-padded; 7% slower from spills) on the same inputs
+        // (round 2, tools/diag/wino3h_modes.py).
         if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
         else if constexpr (K == -1)
             asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
