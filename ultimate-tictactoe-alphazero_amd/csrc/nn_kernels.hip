@@ -5,7 +5,7 @@
 //               planes (own, opponent, legal; uttt_game.cpp:244-280) are 0/1, so the
 //               conv is a masked sum of 27 weight rows; no NCHW tensor is built.
 //   k_heads     1x1 convs (128->2, 128->1) + ReLU, policy FC 162->81 + softmax,
-//               value FC 81->256 + ReLU + FC 256->1 + tanh: four positions per workgroup.
+//               value FC 81->256 + ReLU + FC 256->1 + tanh: one position per workgroup.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -88,8 +88,10 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
 
 // Head weight block (uttt_nn.h UTTT_HEAD_*): folded 1x1 convs, then the FC layers with
 // their weights stored input-major (consecutive threads = consecutive outputs read
-// consecutive floats). HB positions per workgroup share every weight load.
-constexpr int HB = 4;
+// consecutive floats). HB positions per workgroup share every weight load; the kernel is
+// latency-bound (chains of L2 weight loads), so more, smaller workgroups win: 1,344 boards
+// take 120 / 73 / 60 / 53 / 52 us at HB = 16 / 8 / 4 / 2 / 1 (tools/diag/nn_parts.py).
+constexpr int HB = 1;
 __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, const float *__restrict__ hw, int n,
                                                float *__restrict__ policy, float *__restrict__ value, int softmax) {
     __shared__ float s_h[HB][3 * 81];  // relu(1x1 conv): [p0 | p1 | v] x 81 (NCHW flatten order)
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, co
             w2[k] = hw[UTTT_HEAD_VCONV_W + 8 * g + k];
         }
         const float c0 = hw[UTTT_HEAD_PCONV_B], c1 = hw[UTTT_HEAD_PCONV_B + 1], c2 = hw[UTTT_HEAD_VCONV_B];
+#pragma unroll 4
         for (int i = t >> 4; i < nb * 81; i += 16) {
             const float4 *src = reinterpret_cast<const float4 *>(act + ((size_t)b0 * 81 + i) * C + 8 * g);
             const float4 xa = src[0], xb = src[1];
@@ -143,6 +146,9 @@ __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, co
 #pragma unroll
         for (int bi = 0; bi < HB; ++bi) acc[bi] = bt;
         const float *w1 = hw + UTTT_HEAD_VFC1_W + t;  // W1^T [81][256]
+        // unrolled: 9 weight loads in flight instead of one L2 round trip per input (the
+        // accumulation order per board is unchanged)
+#pragma unroll 9
         for (int j = 0; j < 81; ++j) {
             const float wj = w1[j * 256];
 #pragma unroll
@@ -165,6 +171,7 @@ __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, co
 #pragma unroll
         for (int r = 0; r < (HB + 2) / 3; ++r) z[r] = bo;
         const float *wp = hw + UTTT_HEAD_PFC_W + o;  // Wp^T [162][81]
+#pragma unroll 9
         for (int j = 0; j < 162; ++j) {
             const float wj = wp[j * 81];
 #pragma unroll
