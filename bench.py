@@ -64,11 +64,15 @@ def parse():
     ap.add_argument("--evaluator", choices=["fused", "nn", "hash"], default="fused")
     ap.add_argument("--net", choices=["seed0", "calibrated"], default="seed0",
                     help="seed0: the reference's initial best.pth; calibrated: tests/golden/netcal.npz")
-    ap.add_argument("--age", type=int, default=100,
-                    help="moves played before warmup so the timed population mixes all game phases")
+    ap.add_argument("--age", type=int, default=300,
+                    help="moves played before warmup so the timed population mixes all game phases and the "
+                         "evaluation cache is at its steady state (hit rate 35.7%% at 100 moves, 30.1%% at 300, "
+                         "31.8%% at 700)")
     ap.add_argument("--lanes", type=int, default=2,
                     help="engines per GPU, each on its own stream; their network evaluations overlap")
-    ap.add_argument("--cache-log2", type=int, default=21, help="evaluation cache entries (log2); 0 = off")
+    ap.add_argument("--cache-log2", type=int, default=23, help="evaluation cache entries (log2); 0 = off")
+    ap.add_argument("--cache-clear-every", type=int, default=0,
+                    help="moves between evaluation-cache clears (0: never; full probe windows replace entries)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
@@ -195,7 +199,8 @@ def union_ms(intervals):
     return busy + (cur[1] - cur[0] if cur is not None else 0.0)
 
 
-def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, age, warmup, steps, evaluator):
+def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, age, warmup, steps, evaluator,
+               cache_clear_every=0):
     """Continuous self-play of `games` slots on this GPU; returns the timed-window statistics."""
     import torch
     import torch.distributed as dist
@@ -205,7 +210,8 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     from uttt_amd.nnfast import FusedNetworkEvaluator
 
     dev = torch.device("cuda", local)
-    sp = SelfPlay(games, sims, batch, 1.0, device=local, cache_log2=cache_log2, lanes=lanes)
+    sp = SelfPlay(games, sims, batch, 1.0, device=local, cache_log2=cache_log2, lanes=lanes,
+                  cache_clear_every=cache_clear_every)
     conv = {"fused": "wino3h"}.get(evaluator)
     tower_events = []
     if evaluator == "hash":
@@ -358,7 +364,7 @@ def main():
     G, S, B = args.games, args.sims, args.batch
     net0 = random_network(0, dev) if args.net == "seed0" else calibrated_network(NETCAL, dev)
     r = run_config(net0, local, rank, world, G, S, B, args.lanes, args.cache_log2, args.age, args.warmup, args.steps,
-                   args.evaluator)
+                   args.evaluator, args.cache_clear_every)
 
     tot = torch.tensor([float(r["sims"]), r["elapsed"]], dtype=torch.float64, device=dev)
     if world > 1:
@@ -420,7 +426,8 @@ def main():
                             f"tau 1.0, continuous self-play (finished games refilled; population aged "
                             f"{args.age} moves before warmup); one step = one move of every game",
                 "games_per_gpu": G, "sims_per_move": S, "mcts_batch_size": B, "aged_moves": args.age,
-                "eval_cache_log2": args.cache_log2, "lanes_per_gpu": args.lanes,
+                "eval_cache_log2": args.cache_log2, "eval_cache_clear_every": args.cache_clear_every,
+                "lanes_per_gpu": args.lanes,
                 "evaluator": {"fused": "DualNetwork 128f x16 on HIP kernels: stem from bitboards, residual tower as "
                                        "fused Winograd F(3x3,3x3) convs (csrc/wino3h_conv.hip, split-f16 MFMA, f32 "
                                        "accumulation, per-board scaling), heads (csrc/nn_kernels.hip)",

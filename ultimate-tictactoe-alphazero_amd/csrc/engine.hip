@@ -248,21 +248,33 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
 // Wave-level insert of (s -> pol[0..80], v). Lane 0 claims a slot by CAS; the
 // payload is stored at agent scope and drained (s_waitcnt vmcnt(0)) before the
 // flag is published, so a reader on any XCD that sees the flag sees the data.
-// A concurrent insert of the same key may leave a harmless duplicate.
+// A concurrent insert of the same key may leave a harmless duplicate. When all
+// kProbe slots hold other positions, one of them (chosen by the hash) is replaced:
+// claimed 2 -> 1 by CAS, rewritten, republished; a reader copying it meanwhile
+// fails its flag-and-key re-check. Entries are exact, so the table never needs
+// clearing while the evaluator is unchanged: it stays warm across moves.
 __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const float *pol, float v) {
     if (!c.flag) return;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
     if (lane == 0) {
         const uint32_t h = state_hash(s);
+        bool present = false;
         for (int i = 0; i < kProbe; ++i) {
             const uint32_t sl = (h + (uint32_t)i) & c.mask;
             const uint32_t f = ld_agent(c.flag + sl);
-            if (f == 2u && key_is(c, sl, s)) break;
+            if (f == 2u && key_is(c, sl, s)) {
+                present = true;
+                break;
+            }
             if (f == 0u && atomicCAS(c.flag + sl, 0u, 1u) == 0u) {
                 slot = (int)sl;
                 break;
             }
+        }
+        if (slot < 0 && !present) {  // every probe slot taken: replace one
+            const uint32_t sl = (h + (h >> 29)) & c.mask;
+            if (atomicCAS(c.flag + sl, 2u, 1u) == 2u) slot = (int)sl;
         }
     }
     slot = __shfl(slot, 0);

@@ -128,12 +128,12 @@ class SelfPlay:
     last waves on the GPU. Records are unchanged (each game depends only on its id)."""
 
     def __init__(self, slots, evaluate_count=50, batch_size=8, temperature=1.0, device=None, evaluator=None,
-                 model=None, cache_log2=None, cache_clear_every=32, lanes=1, evaluator_kind=None):
+                 model=None, cache_log2=None, cache_clear_every=0, lanes=1, evaluator_kind=None):
         if lanes < 1 or slots % lanes:
             raise ValueError("slots must be a positive multiple of lanes")
         per = slots // lanes
-        if cache_log2 is None:  # ~512 entries per slot: a 32-move window of one game's leaves
-            cache_log2 = min(21, max(12, int(math.ceil(math.log2(max(per, 1)))) + 9))
+        if cache_log2 is None:  # ~2048 entries per slot (2^23 = 3 GB of HBM for 4096 games)
+            cache_log2 = min(23, max(12, int(math.ceil(math.log2(max(per, 1)))) + 11))
         self.lanes = []
         for i in range(lanes):
             self.lanes.append(_Lane(per, evaluate_count, device, cache_log2 if i == 0 else 0, cache_clear_every,
