@@ -99,7 +99,7 @@ struct Trees {
     int32_t *path;    // [tree][kMaxDepth]
     int32_t *pending; // [tree]
     int32_t *tree_of; // [slot]
-    int32_t *count;   // [1] pending leaves this round
+    int32_t *count;   // [0] pending leaves this round, [1] trees stopped by the select budget
     int32_t n_trees;
     int32_t sims;
     int32_t batch;
@@ -466,6 +466,13 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 // Terminal simulations are backed up in place (:115-118). The k-1 further
 // simulations the reference spends re-finding the same queued leaf are
 // accounted by k.
+// A launch lasts as long as its slowest tree's chain of dependent loads, and a tree
+// whose simulations end on terminals or evaluation-cache hits completes them in place,
+// one descent after another. A tree stops after kSelectBudget such completions
+// (pending = 2) and resumes in the next launch from the same point: the sequence of
+// simulations per tree, hence every result, is unchanged; only the tail of the launch is cut.
+constexpr int kSelectBudget = 8;
+
 __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCache cache,
                                                    unsigned long long *stats) {
     __shared__ float s_hit[kWavesPerBlock][kCacheVal];  // a cache hit's values, per wave
@@ -483,6 +490,7 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
         const uint2 *__restrict__ LK = pool.link + base;
         const uttt_state_t root = tr.root[t];
         int sims_done = ctl.sims_done;
+        int budget = kSelectBudget;
         for (;;) {
             uttt_state_t s = root;
             int node = 0, depth = 0;
@@ -585,6 +593,10 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
                 bytes += 16ull * (unsigned long long)(depth + 1);
                 ++sims_done;
                 if (sims_done >= tr.sims) break;
+                if (--budget == 0) {
+                    pend = 2;
+                    break;
+                }
                 continue;
             }
             // Unexpanded leaf (n == 0 && no children, uttt_mcts.cpp:121): queue it with
@@ -602,6 +614,10 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
                 bytes += 20ull * (unsigned long long)(k * meta_L(LK[node].y)) + 16ull * (depth + 1);
                 sims_done += k;
                 if (sims_done >= tr.sims) break;
+                if (--budget == 0) {
+                    pend = 2;
+                    break;
+                }
                 continue;
             }
             if (cache.flag && lane == 0) atomicAdd(cache.ctr + 1, 1ull);
@@ -645,9 +661,16 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);
-    int local = 0;
-    for (int i = b; i < e; ++i) local += tr.pending[i];
+    __shared__ int capped;
+    if (tid == 0) capped = 0;
+    int local = 0, cap = 0;
+    for (int i = b; i < e; ++i) {
+        local += tr.pending[i] == 1;
+        cap += tr.pending[i] == 2;
+    }
     sums[tid] = local;
+    __syncthreads();
+    if (cap) atomicAdd(&capped, cap);
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
         const int v = tid >= off ? sums[tid - off] : 0;
@@ -657,8 +680,11 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     }
     int slot = sums[tid] - local;
     for (int i = b; i < e; ++i)
-        if (tr.pending[i]) tr.tree_of[slot++] = i;
-    if (tid == 1023) tr.count[0] = sums[1023];
+        if (tr.pending[i] == 1) tr.tree_of[slot++] = i;
+    if (tid == 1023) {
+        tr.count[0] = sums[1023];
+        tr.count[1] = capped;
+    }
 }
 
 // ----------------------------------------------------------------- encode --
@@ -1377,7 +1403,7 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     if ((rc = alloc_n(e, &e->tr.ctl, max_trees)) || (rc = alloc_n(e, &e->tr.root, max_trees)) ||
         (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
-        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 1)) ||
+        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 2)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)) ||
         (rc = alloc_n(e, &e->d_cache_ctr, 4)))
@@ -1483,22 +1509,28 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
         return UTTT_ERR_ORDER;
     }
     HIP_TRY(hipSetDevice(e->device));
-    {
-        TimedLaunch tl(e, kKSelect);
-        hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr, e->cache,
-                           e->timing ? e->d_bytes : nullptr);
+    int rc = 0, n = 0;
+    // trees stopped by the select budget resume in the next launch; when no tree has a
+    // leaf but some were stopped, select again (every launch completes >= 1 simulation
+    // of each stopped tree, so this ends)
+    for (;;) {
+        {
+            TimedLaunch tl(e, kKSelect);
+            hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+                               e->cache, e->timing ? e->d_bytes : nullptr);
+        }
+        if ((rc = check_launch())) return rc;
+        {
+            TimedLaunch tl(e, kKScan);
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr);
+        }
+        if ((rc = check_launch())) return rc;
+        HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        drain_events(e);
+        n = e->h_count[0];
+        if (n > 0 || e->h_count[1] == 0) break;
     }
-    int rc = check_launch();
-    if (rc) return rc;
-    {
-        TimedLaunch tl(e, kKScan);
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr);
-    }
-    if ((rc = check_launch())) return rc;
-    HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    drain_events(e);
-    const int n = e->h_count[0];
     if (n > 0 && nn_input) {
         TimedLaunch tl(e, kKEncode);
         const int total = n * 243;
