@@ -312,7 +312,7 @@ def conv_roofline(r):
     achieved = flop / (avg_us * 1e-6) / 1e12
     pmc = newest_profile("pmc_conv.json", {"kernel": "k_wino3h_conv"}) if conv == "wino3h" else None
     traffic = round(pmc["hbm_bytes_per_board"] * boards_per_launch) if pmc else None
-    algo_bytes = CONV_BYTES_PER_BOARD * boards_per_launch + 25 * 128 * 128 * (4 if conv == "wino3h" else 4)
+    algo_bytes = CONV_BYTES_PER_BOARD * boards_per_launch + U_BYTES_PER_SET
     return {"kernel": f"k_{conv}_conv (residual-tower 3x3 conv, Winograd F(3x3,3x3) on the "
                       f"{'f16 MFMA, 3-term split-f16 products, f32 accumulation' if conv == 'wino3h' else 'f32 MFMA'})",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": CONV_PEAK[conv], "unit": "TFLOP/s",
@@ -323,8 +323,32 @@ def conv_roofline(r):
             "avg_launch_us": round(avg_us, 2), "launches": launches, "boards_per_launch": round(boards_per_launch, 1),
             "executed_flop_per_board": CONV_EXEC_FLOP[conv], "direct_equiv_flop_per_board": CONV_DIRECT_FLOP,
             "direct_equiv_tflops": round(CONV_DIRECT_FLOP * boards_per_launch / (avg_us * 1e-6) / 1e12, 1),
+            "vmem_stream": conv_vmem_roofline(r["tower"], avg_us),
             "note": "two lanes' conv launches overlap on the GPU, so each launch's duration includes the time it "
                     "shares the CUs with the other lane's; aggregate = nn.mfma_executed_tflops"}
+
+
+# Measured ceiling of the L2 -> CU vector-memory path for 16-byte lane-linear loads, every CU
+# streaming (tools/diag/u_stream.hip: 95-108 GB/s per CU x 256 CUs); what bounds the conv's
+# point GEMMs
+L2_STREAM_CEILING_TBS = 27.7
+U_BYTES_PER_SET = 25 * 128 * 128 * 4   # every 32-tile set streams all of U (f16 hi + lo) from L2
+
+
+def conv_sets(n):
+    """k_wino3h_conv sets of n boards: two per full group of 7, one or two for a partial group."""
+    return 2 * (n // 7) + (0 if n % 7 == 0 else (1 if n % 7 <= 3 else 2))
+
+
+def conv_vmem_roofline(tower, avg_us):
+    """The conv's binding resource: bytes through each CU's vector-memory path per launch (U once
+    per set, inputs, outputs and residual per board) / launch time, against the measured ceiling."""
+    per_launch = sum(conv_sets(n) * U_BYTES_PER_SET + CONV_BYTES_PER_BOARD * n for n, _ in tower) / len(tower)
+    achieved = per_launch / (avg_us * 1e-6) / 1e12
+    return {"bytes_per_launch": round(per_launch), "achieved": round(achieved, 2), "ceiling": L2_STREAM_CEILING_TBS,
+            "unit": "TB/s", "frac": round(achieved / L2_STREAM_CEILING_TBS, 4),
+            "basis": "U (1.6 MB) streamed from L2 by every 32-tile set + 103.7 KB per board of activations; ceiling "
+                     "= lane-linear 16-B loads with every CU streaming (tools/diag/u_stream.hip)"}
 
 
 def hbm_roofline(name, stat, trees_per_launch, pmc_name=None):
