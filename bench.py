@@ -323,7 +323,7 @@ def conv_roofline(r):
             "avg_launch_us": round(avg_us, 2), "launches": launches, "boards_per_launch": round(boards_per_launch, 1),
             "executed_flop_per_board": CONV_EXEC_FLOP[conv], "direct_equiv_flop_per_board": CONV_DIRECT_FLOP,
             "direct_equiv_tflops": round(CONV_DIRECT_FLOP * boards_per_launch / (avg_us * 1e-6) / 1e12, 1),
-            "vmem_stream": conv_vmem_roofline(r["tower"], avg_us),
+            "vmem_stream": conv_vmem_roofline(r["tower"], avg_us, r["nn_ms"]),
             "note": "two lanes' conv launches overlap on the GPU, so each launch's duration includes the time it "
                     "shares the CUs with the other lane's; aggregate = nn.mfma_executed_tflops"}
 
@@ -340,13 +340,18 @@ def conv_sets(n):
     return 2 * (n // 7) + (0 if n % 7 == 0 else (1 if n % 7 <= 3 else 2))
 
 
-def conv_vmem_roofline(tower, avg_us):
+def conv_vmem_roofline(tower, avg_us, nn_ms):
     """The conv's binding resource: bytes through each CU's vector-memory path per launch (U once
-    per set, inputs, outputs and residual per board) / launch time, against the measured ceiling."""
-    per_launch = sum(conv_sets(n) * U_BYTES_PER_SET + CONV_BYTES_PER_BOARD * n for n, _ in tower) / len(tower)
+    per set, inputs, outputs and residual per board) / launch time, against the measured ceiling.
+    aggregate_*: every conv's bytes over the union of the lanes' forward intervals (stem and heads
+    included, so conservative) -- the rate the chip sustains while two lanes' launches overlap."""
+    per_fwd = [conv_sets(n) * U_BYTES_PER_SET + CONV_BYTES_PER_BOARD * n for n, _ in tower]
+    per_launch = sum(per_fwd) / len(tower)
     achieved = per_launch / (avg_us * 1e-6) / 1e12
+    agg = 32 * sum(per_fwd) / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     return {"bytes_per_launch": round(per_launch), "achieved": round(achieved, 2), "ceiling": L2_STREAM_CEILING_TBS,
             "unit": "TB/s", "frac": round(achieved / L2_STREAM_CEILING_TBS, 4),
+            "aggregate_achieved": round(agg, 2), "aggregate_frac": round(agg / L2_STREAM_CEILING_TBS, 4),
             "basis": "U (1.6 MB) streamed from L2 by every 32-tile set + 103.7 KB per board of activations; ceiling "
                      "= lane-linear 16-B loads with every CU streaming (tools/diag/u_stream.hip)"}
 
