@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
+    # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo instead of RCCL
+    ap.add_argument("--rehearse-shared-gpu", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-baseline-child", choices=["cpu-nn", "tree", "device-nn"], help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -382,11 +384,14 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = 0 if args.rehearse_shared_gpu else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
 
@@ -395,7 +400,8 @@ def main():
     r = run_config(net0, local, rank, world, G, S, B, args.lanes, args.cache_log2, args.age, args.warmup, args.steps,
                    args.evaluator, args.cache_clear_every)
 
-    tot = torch.tensor([float(r["sims"]), r["elapsed"]], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(r["sims"]), r["elapsed"]], dtype=torch.float64,
+                       device="cpu" if args.rehearse_shared_gpu else dev)
     if world > 1:
         s = tot[:1].clone()
         m = tot[1:].clone()
@@ -499,6 +505,8 @@ def main():
                                 log2_capacity=args.cache_log2) if r["cache"] else None),
             "variants": variants,
         }
+        if args.rehearse_shared_gpu:
+            out["config"]["rehearsal"] = f"{world} ranks sharing one GPU over gloo (not a scaling measurement)"
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = run_cpu_baseline("cpu-nn", args.cpu_seconds)
             out["cpu_baselines"] = {"b_tree_all_cores": run_cpu_baseline("tree", 10.0),

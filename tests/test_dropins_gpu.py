@@ -142,6 +142,25 @@ def test_self_play_cpp_sharded_over_two_ranks(gpu, tmp_path):
     _check_history(hist, d, ng)
 
 
+def test_bench_multi_rank_path(gpu):
+    """bench.py's N>1 path (what the driver's scaling run executes) rehearsed with 2 torchrun ranks
+    on the one GPU (gloo instead of RCCL): per-rank game blocks, barrier + max-over-ranks timing,
+    the whole-job value and one JSON line from rank 0."""
+    import json
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--age", "3", "--games", "256",
+           "--rehearse-shared-gpu", "--no-variants", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and "rehearsal" in out["config"]
+    # 2 ranks x 256 games x 50 sims per step, whole-job over the slowest rank's time
+    assert out["value"] > 0 and abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 256 * 50) < 1e-3 * 2 * 256 * 50
+
+
 def test_mini_train_cycle(gpu, tmp_path, monkeypatch):
     """train_cycle.py:21-39 in miniature, every step through this build's drop-ins in a fresh
     working directory: dual_network() -> self_play() (fused evaluator, .history) ->
