@@ -46,6 +46,9 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(n)
         x = torch.relu(torch.randn(n, 81, 128, device="cuda", generator=g))
         ba = board_amax(x)
+        # residual-form modes (bit 20) read a separate tensor, as the tower's block input is
+        r = torch.relu(torch.randn(n, 81, 128, device="cuda", generator=g))
+        lib.uttt_diag_wino3h_set_residual(_p(r))
         y0 = torch.empty_like(x)
         t_prod = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y0),
                                                           _p(ba), 1, None, None, 0, n, st))

@@ -406,10 +406,15 @@ __device__ __forceinline__ SetScale set_scale(const uint32_t *__restrict__ x_ama
 __device__ unsigned int g_stamp[64][2][8][6];
 
 // MODE (timing ablations only; 0 in the product): 1 skip the transform, 2 skip the
-// point GEMMs, 64 skip the fold, 512 plain (L2-allocating) activation loads/stores.
-// The product streams activations with nontemporal loads/stores: each is touched once
-// per launch and would otherwise evict U (1.6 MB, re-read per set) from the XCD's L2
-// (-4..6% at bench batch sizes, tools/diag/wino3h_time.py).
+// point GEMMs, 64 skip the fold, 512 plain (L2-allocating) input loads, 65536 nontemporal
+// residual loads, 131072 nontemporal output stores.
+// The product streams the conv input with nontemporal loads: 8 lanes read one whole 128-B
+// line, each line once per launch, and L2-allocating them would evict U (1.6 MB, re-read
+// per set) from the XCD's L2 (-4..6% at bench batch sizes). The epilogue's residual loads
+// and output stores are plain: one wave covers 64 B (16 channels) of a position's 512-B
+// row, so the two waves that share a 128-B line meet in L2 instead of each moving the line
+// to or from HBM (residual conv 106.7 -> 91.0 us at 1,344 boards, round 2,
+// tools/diag/wino3h_modes.py).
 template <bool RES, int MODE = 0, int PF = 3>
 __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
                                                     float u_scale, const float *__restrict__ bias,
@@ -527,7 +532,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                         rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
                         if (live[rt]) {
                             const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
-                            rv[ab] = (MODE & 512) ? *src : __builtin_nontemporal_load(src);
+                            rv[ab] = (MODE & 65536) ? __builtin_nontemporal_load(src) : *src;
                         }
                     }
                 }
@@ -563,7 +568,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                     floatx4 *dst = reinterpret_cast<floatx4 *>(y + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
                     if constexpr (MODE & 8) {  // diagnostic: no output stores (kept live)
                         asm volatile("" ::"v"(v));
-                    } else if constexpr (!(MODE & 512)) {
+                    } else if constexpr (MODE & 131072) {
                         __builtin_nontemporal_store(v, dst);
                     } else {
                         *dst = v;
@@ -613,6 +618,16 @@ static int grid_size(int n_boards) {
 }  // namespace uttt
 
 using namespace uttt;
+
+// diagnostic: the residual form of an ablation launch (residual = g_diag_res if set, else x)
+static const float *g_diag_res = nullptr;
+template <int MODE>
+static void ablation_res(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
+                         const uint32_t *x_amax, int32_t n_boards, hipStream_t st) {
+    using namespace wino3h;
+    hipLaunchKernelGGL((k_wino3h_conv<true, MODE>), dim3(grid_size(n_boards)), dim3(NT), 0, st, x, u, u_scale, bias,
+                       g_diag_res ? g_diag_res : x, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+}
 
 extern "C" {
 
@@ -719,13 +734,27 @@ int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream) {
     return UTTT_OK;
 }
 
+// Diagnostic: the residual tensor of the ablation's residual form (null: x itself)
+void uttt_diag_wino3h_set_residual(const float *res) { g_diag_res = res; }
+
 // Diagnostic (not declared in uttt_nn.h): the same launch with a timing ablation.
 int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
                               const uint32_t *x_amax, int32_t n_boards, int32_t mode, void *stream) {
     const dim3 grid(wino3h::grid_size(n_boards));
     hipStream_t st = (hipStream_t)stream;
     using namespace wino3h;
+    if (mode & (1 << 20)) {  // the residual form (residual = x)
+        switch (mode & ~(1 << 20)) {
+            case 65536: ablation_res<65536>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case 131072: ablation_res<131072>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case 196608: ablation_res<196608>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case 8: ablation_res<8>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            default: ablation_res<0>(x, u, u_scale, bias, y, x_amax, n_boards, st);
+        }
+        return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+    }
     switch (mode) {
+        case 131072: hipLaunchKernelGGL((k_wino3h_conv<false, 131072>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
         case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
