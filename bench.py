@@ -20,6 +20,7 @@ the CPU baselines (`cpu_baseline`: the reference's own C++ search with its
 DualNetwork on the host cores; `cpu_baselines`: BASELINE.md's B-tree and B-e2e).
 """
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -76,6 +77,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the isolated conv timing after the timed region (rocprof window runs)")
     # rehearsal of the multi-rank path on a one-GPU box: every rank on device 0, gloo instead of RCCL
     ap.add_argument("--rehearse-shared-gpu", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-baseline-child", choices=["cpu-nn", "tree", "device-nn"], help=argparse.SUPPRESS)
@@ -330,6 +333,53 @@ def conv_roofline(r):
                     "shares the CUs with the other lane's; aggregate = nn.mfma_executed_tflops"}
 
 
+def isolated_conv(net, boards_list, reps=20):
+    """The dominant kernel alone on the GPU (after the timed region, no other lane): the product
+    launch of one tower conv (block 8's conv1 weights, plain and residual forms alternating as in
+    the tower) on random post-ReLU inputs of n boards, HIP events on the launching stream around
+    `reps` launches. Gives the kernel's own roofline beside the in-bench figure, whose launches
+    share the CUs with the other lane's."""
+    import torch
+    from uttt_amd.model import fold_bn
+    from uttt_amd.nnfast import board_amax, wino3h_weights, _p
+    from uttt_amd import _lib
+    lib = _lib.load()
+    w, b = fold_bn(net.residual_blocks[8].conv1, net.residual_blocks[8].bn1)
+    uh, su = wino3h_weights(w)
+    uh, b = uh.cuda(), b.float().contiguous().cuda()
+    stream = torch.cuda.current_stream()
+    st = ctypes.c_void_p(stream.cuda_stream)
+    out = []
+    for n in boards_list:
+        g = torch.Generator(device="cuda").manual_seed(n)
+        x = torch.relu(torch.randn(n, 81, 128, device="cuda", generator=g))
+        res = torch.relu(torch.randn(n, 81, 128, device="cuda", generator=g))
+        y = torch.empty_like(x)
+        ba = board_amax(x)
+
+        def launch(i):
+            rc = lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(res) if i & 1 else None,
+                                            _p(y), _p(ba), 1, None, None, 0, n, st)
+            if rc != 0:
+                raise RuntimeError(f"uttt_nn_conv3x3_wino3h failed ({rc})")
+        for i in range(4):
+            launch(i)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(reps):
+            launch(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        tf = CONV_EXEC_FLOP["wino3h"] * n / (us * 1e-6) / 1e12
+        out.append({"boards": n, "avg_launch_us": round(us, 2), "achieved": round(tf, 2),
+                    "frac": round(tf / CONV_PEAK["wino3h"], 4)})
+        del x, res, y
+    return {"unit": "TFLOP/s", "peak": CONV_PEAK["wino3h"], "points": out,
+            "basis": "one launch at a time, no other lane (block 8 conv1 weights, random post-ReLU inputs, plain and "
+                     "residual forms alternating); the headline roofline above is the in-bench figure"}
+
+
 # Measured ceiling of the L2 -> CU vector-memory path for 16-byte lane-linear loads, every CU
 # streaming (tools/diag/u_stream.hip: 95-108 GB/s per CU x 256 CUs); what bounds the conv's
 # point GEMMs (DESIGN.md §5)
@@ -427,6 +477,11 @@ def main():
             sv["conv_roofline_frac"] = (conv_roofline(rv) or {}).get("frac")
             variants[key] = sv
 
+    iso = None
+    if world == 1 and not args.no_isolated and r["conv"] == "wino3h" and r["tower"]:
+        nb = round(sum(n for n, _ in r["tower"]) / len(r["tower"]))
+        iso = isolated_conv(net0, [nb, 16384])
+
     if rank == 0:
         value = total_sims / max_elapsed
         st = r["stats"]
@@ -505,6 +560,8 @@ def main():
                                 log2_capacity=args.cache_log2) if r["cache"] else None),
             "variants": variants,
         }
+        if iso and out.get("roofline") and out["roofline"].get("bound") == "mfma":
+            out["roofline"]["isolated"] = iso
         if args.rehearse_shared_gpu:
             out["config"]["rehearsal"] = f"{world} ranks sharing one GPU over gloo (not a scaling measurement)"
         if world == 1 and not args.no_cpu_baseline:

@@ -22,7 +22,7 @@ rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/$TAG/bench.log | cut -c1-400
 [ $rc -eq 0 ] || exit $rc
 if [ -z "${SKIP_PROF:-}" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/prof -o bench \
-      -- python3 bench.py --no-cpu-baseline --no-variants ${BENCH_ARGS:-} > gpurun_out/$TAG/prof_bench.log 2>&1
+      -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > gpurun_out/$TAG/prof_bench.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -1 gpurun_out/$TAG/prof_bench.log | cut -c1-300
 fi
 exit $rc
