@@ -73,6 +73,8 @@ constexpr int VB = NP * 4 * VPLANE;              // V bytes: [xi][rt][h][kq][row
 constexpr int XF4 = SB * 81 * (KC / 4);          // float4s staged per chunk (2592)
 constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (6)
 static_assert(NITEM == NT, "one transform item per thread");
+constexpr int NPAD = XP - SB * 81;  // zero positions of the staged layout (87)
+static_assert(NPAD == 5 * 10 + 4 * 9 + 1, "pad positions: shared zero rows, zero column, last position");
 static_assert(XP * KC * 4 + VB <= 160 * 1024, "LDS");
 
 // Sets of n boards: two per full group of 7, one or two for a partial last group
@@ -462,8 +464,14 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     // MI355X_MICROARCH.md §LDS); m ^ 4kq made the reads 2-way
     const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (2 * kq)) * 16);
 
-    // zero the pads of sX (never written after this)
-    for (int i = tid; i < XP * KC; i += NT) sX[i] = 0.0f;
+    // zero the pads of sX (never written after this; the staged cells are rewritten every chunk):
+    // the 5 shared zero rows (10 positions each), the zero column of the 36 board rows, the last position
+    for (int i = tid; i < NPAD * (KC / 4); i += NT) {
+        const int j = i / (KC / 4), q = i % (KC / 4);
+        const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
+                      : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
+        reinterpret_cast<float4 *>(sX + pos * KC)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
     __syncthreads();
     BFrag bq[PF];
 #pragma unroll
