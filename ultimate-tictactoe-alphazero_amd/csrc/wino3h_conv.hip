@@ -466,7 +466,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
 
     // zero the pads of sX (never written after this; the staged cells are rewritten every chunk):
     // the 5 shared zero rows (10 positions each), the zero column of the 36 board rows, the last position
-    for (int i = tid; i < NPAD * (KC / 4); i += NT) {
+    for (int i = fresh(tid); i < NPAD * (KC / 4); i += NT) {
         const int j = i / (KC / 4), q = i % (KC / 4);
         const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
                       : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
