@@ -35,7 +35,8 @@
 // barrier, then all waves run the 25 point GEMMs M^T = U^T V^T (U fragments from
 // L2 a few points ahead as the A operand, V from LDS as the B operand, so a lane's
 // four results are four consecutive output channels of one tile) with the previous
-// point's fold (S[a][v] += A^T[a][u] M) spread over the next point's MFMAs; the
+// point's fold (S[a][v] += A^T[a][u] M) spread over the next point's MFMAs (points
+// u = 0 and 4 accumulate into S on the MFMA itself); the
 // next chunk's inputs are in flight meanwhile. Y = S A after a set's last chunk,
 // then scale, bias, residual, ReLU, and one 16-byte store per output position
 // straight from registers, output max.
@@ -103,10 +104,16 @@ __host__ __device__ constexpr int nth_row(int u, int i) {
     return a;
 }
 
+// Points whose A^T column has one nonzero (u = 0 -> row 0, u = 4 -> row 2, both coefficient 1)
+// accumulate straight into their S row as the MFMA's C operand: no fold ops for 10 of the 25
+// points (40 of 220 packed adds per chunk; 2-10% per launch, round 2)
+template <int P, int MODE>
+__host__ __device__ constexpr bool acc_direct() { return n_rows(P / 5) == 1; }
+
 template <int P, int O, int MODE>
 __device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
     constexpr int u = P / 5, v = P % 5;
-    if constexpr (O < 4 * n_rows(u)) {
+    if constexpr (O < 4 * n_rows(u) && !acc_direct<P, MODE>()) {
         constexpr int a = nth_row(u, O / 4), j = O % 4, K = at(a, u);
         // Inline asm is outside the compiler's hazard recognizer, so nothing pads these reads of
         // the previous point's MFMA results; the schedule keeps >= 6 instructions, one of them an
@@ -202,6 +209,11 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             }
             __builtin_amdgcn_sched_barrier(0);
             floatx4 m0 = {}, m1 = {};
+            constexpr int srow = nth_row(XI / 5, 0) * 5 + XI % 5;  // the S row of a direct point
+            if constexpr (acc_direct<XI, MODE>()) {
+                m0 = floatx4{S[srow].p[0].x, S[srow].p[0].y, S[srow].p[1].x, S[srow].p[1].y};
+                m1 = floatx4{S[srow].p[2].x, S[srow].p[2].y, S[srow].p[3].x, S[srow].p[3].y};
+            }
             constexpr bool fold_here = XI > 0 && !(MODE & 64);
             // small terms first, then the hi x hi product
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h0, m0, 0, 0, 0);
@@ -217,6 +229,12 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
             if constexpr (fold_here) fold_slot<XI - 1, 5, MODE>(S, mprev, k2, k4);
             asm volatile("" : "+v"(m0), "+v"(m1));  // keep this point's MFMAs in its own region
+            if constexpr (acc_direct<XI, MODE>()) {
+                S[srow].p[0] = __builtin_shufflevector(m0, m0, 0, 1);
+                S[srow].p[1] = __builtin_shufflevector(m0, m0, 2, 3);
+                S[srow].p[2] = __builtin_shufflevector(m1, m1, 0, 1);
+                S[srow].p[3] = __builtin_shufflevector(m1, m1, 2, 3);
+            }
             m[0] = __builtin_shufflevector(m0, m0, 0, 1);
             m[1] = __builtin_shufflevector(m0, m0, 2, 3);
             m[2] = __builtin_shufflevector(m1, m1, 0, 1);
@@ -524,7 +542,9 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                 const int gt = 32 * h + 16 * rt + (el & 15), gb = gt / 9, tt = gt - 9 * gb;
                 const int board = GB * grp + gb;
                 live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
-                off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4;
+                // this lane's 4 output channels, recomputed here rather than kept live (spilled) over the loop
+                const int co4e = (fresh(tid) >> 6) * 16 + 4 * (el >> 4);
+                off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4e;
                 board_of[rt] = board;
                 // this tile's board's V scale times su: both powers of two, so 1/x is exact
                 inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
