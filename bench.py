@@ -465,16 +465,32 @@ def main():
         variants = {}
         for key, kw in (("calibrated_net", dict(net=calibrated_network(NETCAL, dev))),
                         ("cache_off", dict(cache_log2=0)),
-                        ("c3_4096x400", dict(sims=400, age=30, warmup=2, steps=4))):
+                        ("c3_4096x400", dict(sims=400, age=30, warmup=2, steps=4)),
+                        # BASELINE configs[1]: 1,024 games x 50 sims, MCTS_BATCH_SIZE 1024 (one flush per move)
+                        ("c2_1024x50_b1024", dict(games=1024, batch=1024, age=100)),
+                        # SURVEY §8(d) kernel microbench: the search kernels alone (hash evaluator, no network)
+                        ("tree_only_4096x50", dict(evaluator="hash", age=100)),
+                        ("tree_only_4096x400", dict(evaluator="hash", sims=400, age=30, warmup=2, steps=4))):
             cfg = dict(net=net0, games=G, sims=S, batch=B, lanes=args.lanes, cache_log2=args.cache_log2,
                        age=args.age, warmup=3, steps=10, evaluator=args.evaluator)
             cfg.update(kw)
             rv = run_config(cfg["net"], local, 0, 1, cfg["games"], cfg["sims"], cfg["batch"], cfg["lanes"],
                             cfg["cache_log2"], cfg["age"], cfg["warmup"], cfg["steps"], cfg["evaluator"])
             sv = summarize(rv, cfg["steps"])
-            sv["config"] = {k: cfg[k] for k in ("games", "sims", "batch", "lanes", "cache_log2", "age", "steps")}
+            sv["config"] = {k: cfg[k] for k in ("games", "sims", "batch", "lanes", "cache_log2", "age", "steps",
+                                                "evaluator")}
             sv["net"] = "calibrated (tests/golden/netcal.npz)" if key == "calibrated_net" else args.net
-            sv["conv_roofline_frac"] = (conv_roofline(rv) or {}).get("frac")
+            if cfg["evaluator"] == "hash":
+                sv["net"] = None
+                sv["roofline_select"] = hbm_roofline("k_select", rv["stats"]["select"], rv["trees_per_launch"])
+                sv["roofline_backup"] = hbm_roofline("k_apply", rv["stats"]["apply"], rv["trees_per_launch"])
+                sv["breakdown_ms"] = {k: round(rv["stats"][k]["ms"], 2) for k in ("select", "apply", "scan", "move_end")}
+                sv["breakdown_ms"]["evaluator"] = round(rv["nn_ms"], 2)
+                sv["breakdown_ms"]["wall"] = round(rv["elapsed"] * 1e3, 2)
+                sv["note"] = ("hash evaluator in place of the network: the search kernels' own rate, to set beside "
+                              "cpu_baselines.b_tree_all_cores (the reference's C++ search with the same evaluator)")
+            else:
+                sv["conv_roofline_frac"] = (conv_roofline(rv) or {}).get("frac")
             variants[key] = sv
 
     iso = None

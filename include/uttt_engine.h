@@ -201,6 +201,10 @@ int uttt_engine_set_cache(uttt_engine_t *eng, int32_t log2_capacity, int32_t cle
 int uttt_engine_cache_clear(uttt_engine_t *eng);
 /* hits: leaves resolved from the table; misses: leaves sent to the evaluator. */
 int uttt_engine_cache_stats(uttt_engine_t *eng, int64_t *hits, int64_t *misses, int64_t *inserts);
+/* The same plus replacements: inserts that found every probe slot holding another position and
+ * rewrote one of them (a full probe window; readers of the old entry retry). */
+int uttt_engine_cache_stats2(uttt_engine_t *eng, int64_t *hits, int64_t *misses, int64_t *inserts,
+                             int64_t *replacements);
 
 /* ------------------------------------------------------------ telemetry --- */
 /* Per-kernel timing with HIP events on the engine's stream (off by default). */

@@ -321,8 +321,52 @@ def _fused_vs_cpu(gpu, bs, roots, fused, cpu, saturated):
         e.apply(p, v2)
 
 
-@pytest.mark.parametrize("netkind", ["seed0", "calibrated"])
-def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib, netkind):
+@pytest.fixture(scope="module")
+def trained_net(gpu):
+    """The seed-0 DualNetwork after ~300 Adam steps of this build's train_network (HIP-graph step,
+    batch 128) on a learnable history: 64 self-play games of the engine with the hash evaluator
+    (policy targets = search visit distributions). Weights, BatchNorm statistics and so the
+    split-f16 kernels' weight-derived scales (U scale per conv, stem bound) are those of a trained
+    net, not of the initialisation."""
+    import torch
+    from uttt_amd import train
+    from uttt_amd.model import random_network
+    sp = gpu.SelfPlay(64, 50, 8, 1.0)
+    sp.run(0, 64, 2024)
+    hist = gpu.history_from_records(sp.records())
+    net = random_network(0, "cuda").train()
+    epochs = max(1, -(-300 // -(-len(hist) // train.BATCH_SIZE)))
+    losses = train.train_network(net, hist, epochs=epochs, device=torch.device("cuda", 0), log=None)
+    assert losses[-1] < losses[0], losses  # it learned something
+    return net.eval(), losses
+
+
+def test_fused_matches_fp32_on_trained_net(gpu, trained_net):
+    """The north star's 1e-5 network bound on TRAINED weights: the fused evaluator (split-f16
+    tower with the trained net's weight-derived scales) against the same model's own fp32
+    PyTorch forward on the CPU, on the netcal positions (dual_network.py:89-121): value and every
+    post-softmax policy entry within 1e-5 absolute."""
+    import copy
+
+    import torch
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    net, _ = trained_net
+    d = golden("netcal.npz")
+    states = _rules_states(d["rules_index"])
+    fe = FusedNetworkEvaluator(net, None, max_batch=len(states))
+    p, v = fe.forward_states(states)
+    cpu = copy.deepcopy(net).cpu().eval()
+    with torch.no_grad():
+        pr, vr = cpu(torch.from_numpy(d["x"].astype(np.float32)))
+    ep = float((p.cpu() - pr).abs().max())
+    ev = float((v.cpu() - vr.reshape(-1)).abs().max())
+    assert ev <= 1e-5 and ep <= 1e-5, (ep, ev)
+    # not saturated: the comparison is not hidden behind tanh / softmax clamping
+    assert float(vr.abs().max()) < 0.999 and float(pr.max(dim=1).values.median()) < 0.9
+
+
+@pytest.mark.parametrize("netkind", ["seed0", "calibrated", "trained"])
+def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib, netkind, request):
     """Search with the fused evaluator; its outputs replayed into the oracle give
     the same root visit counts."""
     from uttt_amd.model import calibrated_network, random_network
@@ -330,7 +374,10 @@ def test_fused_evaluator_search_replays_exactly(gpu, oracle_lib, netkind):
     core = oracle_lib
     roots, ostates = _random_positions(core, 48, seed=17)
     bs = gpu.BatchedSearch(len(roots), 50)
-    net = random_network(0, "cuda") if netkind == "seed0" else calibrated_network(NETCAL, "cuda")
+    if netkind == "trained":
+        net = request.getfixturevalue("trained_net")[0]
+    else:
+        net = random_network(0, "cuda") if netkind == "seed0" else calibrated_network(NETCAL, "cuda")
     fused = FusedNetworkEvaluator(net, bs.engine)
     table = {}
 
@@ -369,6 +416,33 @@ def test_fused_selfplay_lanes_are_bit_identical(gpu):
     a = out[0]
     for b in out[1:]:
         assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(12))
+        for ra, rb in zip(a, b):
+            assert np.array_equal(ra["actions"], rb["actions"])
+            assert np.array_equal(ra["policies"].view(np.uint64), rb["policies"].view(np.uint64))
+            assert np.array_equal(ra["values"], rb["values"])
+
+
+def test_eval_cache_replacement_is_exact(gpu):
+    """A tiny shared table (2^6 entries for 32 trees, two lanes on two streams): nearly every
+    insert finds its 8 probe slots taken and replaces an entry another lane may be reading
+    (cache_insert CAS 2 -> 1, rewrite, republish; cache_lookup re-checks flag and key after its
+    drained payload loads). Records equal the no-cache run bit for bit, hits and replacements
+    both happen."""
+    from uttt_amd.model import calibrated_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    net = calibrated_network(NETCAL, "cuda")
+    out, stats = [], []
+    for lanes, cache in ((1, 0), (2, 6), (2, 7)):
+        sp = gpu.SelfPlay(32, 50, 8, 1.0, lanes=lanes, cache_log2=cache)
+        sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng))
+        sp.run(0, 24, 99)
+        out.append(sp.records())
+        stats.append(sp.cache_stats())
+    for st in stats[1:]:
+        assert st["replacements"] > 0 and st["hits"] > 0 and st["inserts"] > (1 << 7), st
+    a = out[0]
+    for b in out[1:]:
+        assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(24))
         for ra, rb in zip(a, b):
             assert np.array_equal(ra["actions"], rb["actions"])
             assert np.array_equal(ra["policies"].view(np.uint64), rb["policies"].view(np.uint64))

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-3 GPU session. STEPS (default "tests smoke train cycle bench") picks the steps, in this order:
+#   tests  every -m gpu test (verbose, per-test timeout)     smoke  __graft_entry__.smoke()
+#   train  tools/bench_train.py (eager / HIP graph / graph + channels-last)
+#   cycle  tools/bench_cycle.py (BASELINE configs[4] on one GPU)
+#   hist   tools/bench_history.py (.history path at C4 scale)
+#   bench  bench.py (headline, variants, CPU baselines)     prof  bench under rocprofv3 --kernel-trace --stats
+# Each GPU step has its own time limit; the session stops at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r3}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+STEPS=${STEPS:-"tests smoke train cycle bench"}
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 240 --timeout-method thread ${PYTEST_K:-} \
+               > $OUT/gputests.log 2>&1 ;;
+    smoke) timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
+    train) timeout -k 10 400 python -u tools/bench_train.py ${TRAIN_ARGS:-} > $OUT/train.log 2>&1 ;;
+    cycle) timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle.json ${CYCLE_ARGS:-} > $OUT/cycle.log 2>&1 ;;
+    hist)  timeout -k 10 300 python -u tools/bench_history.py > $OUT/history.log 2>&1 ;;
+    bench) timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 ;;
+    prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
+               -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/prof_bench.log 2>&1 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  rc=$?
+  echo "== $s rc=$rc"
+  log=$(ls -t $OUT/*.log | head -1)
+  tail -3 "$log" | cut -c1-600
+  [ $rc -eq 0 ] || exit $rc
+done
+exit 0

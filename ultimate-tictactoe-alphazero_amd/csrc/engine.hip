@@ -173,7 +173,7 @@ struct EvalCache {
     uttt_state_t *key;
     float *val;          // [slot][82]
     uint32_t mask;       // capacity - 1
-    unsigned long long *ctr;  // [0] hits, [1] misses (network leaves), [2] inserts
+    unsigned long long *ctr;  // [0] hits, [1] misses (network leaves), [2] inserts, [3] replacements
 };
 
 __device__ __forceinline__ uint32_t state_hash(const uttt_state_t &s) {
@@ -237,6 +237,10 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
     const float *src = c.val + (size_t)hs * kCacheVal;
     const float v0 = ld_agent(src + lane);
     const float v1 = lane < kCacheVal - 64 ? ld_agent(src + 64 + lane) : 0.0f;
+    // seqlock read side: the payload loads must be served before the re-check below is
+    // issued, or the re-check could see the old flag and key while the payload loads see a
+    // replacement in progress (cache_insert: CAS 2 -> 1, rewrite, republish)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bool ok = true;
     if (lane == 0) ok = ld_agent(c.flag + hs) == 2u && key_is(c, hs, s);
     if (!__shfl(ok, 0)) return false;
@@ -274,7 +278,10 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
         }
         if (slot < 0 && !present) {  // every probe slot taken: replace one
             const uint32_t sl = (h + (h >> 29)) & c.mask;
-            if (atomicCAS(c.flag + sl, 2u, 1u) == 2u) slot = (int)sl;
+            if (atomicCAS(c.flag + sl, 2u, 1u) == 2u) {
+                slot = (int)sl;
+                atomicAdd(c.ctr + 3, 1ull);
+            }
         }
     }
     slot = __shfl(slot, 0);
@@ -1929,10 +1936,18 @@ int uttt_engine_cache_clear(uttt_engine_t *e) {
     if (!e->cache.flag || !e->cache_owner) return UTTT_OK;
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemsetAsync(e->cache.flag, 0, sizeof(uint32_t) * ((size_t)1 << e->cache_log2), e->stream));
+    // engines sharing the table launch on their own streams: nothing would order their next
+    // lookups after this clear, so it completes before the call returns (once per run)
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return UTTT_OK;
 }
 
 int uttt_engine_cache_stats(uttt_engine_t *e, int64_t *hits, int64_t *misses, int64_t *inserts) {
+    return uttt_engine_cache_stats2(e, hits, misses, inserts, nullptr);
+}
+
+int uttt_engine_cache_stats2(uttt_engine_t *e, int64_t *hits, int64_t *misses, int64_t *inserts,
+                             int64_t *replacements) {
     if (!e) return UTTT_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
     unsigned long long c[4];
@@ -1941,6 +1956,7 @@ int uttt_engine_cache_stats(uttt_engine_t *e, int64_t *hits, int64_t *misses, in
     if (hits) *hits = (int64_t)c[0];
     if (misses) *misses = (int64_t)c[1];
     if (inserts) *inserts = (int64_t)c[2];
+    if (replacements) *replacements = (int64_t)c[3];
     return UTTT_OK;
 }
 

@@ -22,6 +22,7 @@ Same names and constants (self_play_cpp.py:26-31), same .history schema
 import os
 import pickle
 import sys
+import time
 from datetime import datetime
 
 import numpy as np
@@ -38,6 +39,7 @@ except ImportError:
 
 from uttt_amd.model import DualNetwork  # noqa: E402
 from uttt_amd.distributed import broadcast_int, init_from_env, self_play_sharded  # noqa: E402
+from uttt_amd.history import write_history_file  # noqa: E402
 from uttt_amd.selfplay import SelfPlay, default_lanes, history_from_records  # noqa: E402
 
 SP_GAME_COUNT = 500
@@ -47,6 +49,8 @@ MCTS_BATCH_SIZE = 8
 
 device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
 _single = {}
+# wall-clock seconds of the last self_play() call's phases (tools/bench_cycle.py)
+LAST_TIMINGS = {}
 
 
 def _fingerprint(model):
@@ -80,13 +84,26 @@ def play(model, use_cpp=True):
     return history_from_records(r.records())
 
 
-def write_history(history, out_dir="./data"):
+def _history_path(out_dir):
     now = datetime.now()
     os.makedirs(out_dir, exist_ok=True)
-    path = os.path.join(out_dir, "{:04}{:02}{:02}{:02}{:02}{:02}.history".format(
+    return os.path.join(out_dir, "{:04}{:02}{:02}{:02}{:02}{:02}.history".format(
         now.year, now.month, now.day, now.hour, now.minute, now.second))
+
+
+def write_history(history, out_dir="./data"):
+    """A history list -> ./data/YYYYmmddHHMMSS.history (self_play_cpp.py:125-130)."""
+    path = _history_path(out_dir)
     with open(path, mode="wb") as f:
         pickle.dump(history, f)
+    return path
+
+
+def write_history_records(records, out_dir="./data"):
+    """The same file from game records, written by uttt_amd.history (loads to the list write_history
+    would store, without pickling ply by ply)."""
+    path = _history_path(out_dir)
+    write_history_file(records, path)
     return path
 
 
@@ -113,22 +130,32 @@ def self_play(use_cpp=True, n_games=None, slots=None, seed_base=None, model_path
         if rank == 0:
             print(f"\rSelfPlay {done}/{total} (Backend: HIP, {world} GPU)", end="")
 
+    LAST_TIMINGS.clear()
+    t0 = time.perf_counter()
     if world > 1:
         recs = self_play_sharded(model, n_games, slots, seed_base, PV_EVALUATE_COUNT, MCTS_BATCH_SIZE,
-                                 SP_TEMPERATURE, lanes=lanes, progress=progress)
+                                 SP_TEMPERATURE, lanes=lanes, progress=progress, timings=LAST_TIMINGS)
     else:
         n_lanes = default_lanes(slots) if lanes is None else lanes
         r = SelfPlay(slots, PV_EVALUATE_COUNT, MCTS_BATCH_SIZE, SP_TEMPERATURE, device=dev.index, model=model,
                      lanes=n_lanes)
-        r.run(0, n_games, seed_base, progress)
+        LAST_TIMINGS["setup_s"] = time.perf_counter() - t0
+        LAST_TIMINGS["games_s"] = r.run(0, n_games, seed_base, progress)
+        LAST_TIMINGS["sims"] = r.sims
+        t1 = time.perf_counter()
         recs = r.records()
+        LAST_TIMINGS["records_s"] = time.perf_counter() - t1
     path = None
     if rank == 0:
         print("")
-        path = write_history(history_from_records(recs), out_dir)
+        t1 = time.perf_counter()
+        path = write_history_records(recs, out_dir)
+        LAST_TIMINGS.update(history_write_s=time.perf_counter() - t1, plies=sum(len(r["actions"]) for r in recs),
+                            history_bytes=os.path.getsize(path))
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+    LAST_TIMINGS["total_s"] = time.perf_counter() - t0
     return path
 
 

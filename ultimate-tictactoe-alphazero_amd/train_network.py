@@ -8,6 +8,7 @@ trains data-parallel over N GPUs with the same global batch
 import os
 import pickle
 import sys
+import time
 from pathlib import Path
 
 import numpy as np
@@ -44,6 +45,10 @@ class HistoryDataset(torch.utils.data.Dataset):
         return self.xs[idx], self.y_policies[idx], self.y_values[idx]
 
 
+# wall-clock seconds of the last train_network() call's phases (tools/bench_cycle.py)
+LAST_TIMINGS = {}
+
+
 def train_network():
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
     if distributed and not dist.is_initialized():
@@ -51,13 +56,22 @@ def train_network():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    LAST_TIMINGS.clear()
+    t0 = time.perf_counter()
     history = load_data()
+    t1 = time.perf_counter()
     model = DualNetwork().to(dev)
     model.load_state_dict(torch.load("./model/best.pth", map_location=dev, weights_only=True))
-    _train.train_network(model, history, RN_EPOCHS, BATCH_SIZE, dev)
+    losses = _train.train_network(model, history, RN_EPOCHS, BATCH_SIZE, dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
     if not distributed or dist.get_rank() == 0:
         torch.save(model.state_dict(), "./model/latest.pth")
         print("Model saved to ./model/latest.pth")
+    LAST_TIMINGS.update(load_s=t1 - t0, train_s=t2 - t1, save_s=time.perf_counter() - t2, samples=len(history),
+                        epochs=RN_EPOCHS, first_loss=losses[0] if losses else None,
+                        last_loss=losses[-1] if losses else None)
     del model
 
 

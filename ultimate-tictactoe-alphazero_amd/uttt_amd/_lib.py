@@ -87,6 +87,7 @@ SIGNATURES = {
     "uttt_engine_set_cache": (ctypes.c_int, [_P, _I32, _I32]),
     "uttt_engine_cache_clear": (ctypes.c_int, [_P]),
     "uttt_engine_cache_stats": (ctypes.c_int, [_P, _I64P, _I64P, _I64P]),
+    "uttt_engine_cache_stats2": (ctypes.c_int, [_P, _I64P, _I64P, _I64P, _I64P]),
     "uttt_nn_stem": (ctypes.c_int, [_P, _P, _P, _P]),
     "uttt_nn_stem_states": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P]),
     "uttt_nn_heads": (ctypes.c_int, [_P, _P, _I32, _P, _P, _I32, _P]),

@@ -11,6 +11,8 @@ reads only the newest file, so it must be one file).
 Compact record per ply: packed state (32 B) + policy target (81 f64) +
 action (i8) + value (i8) + game id (i64) = 690 B.
 """
+import time
+
 import numpy as np
 
 from ._lib import STATE_DTYPE
@@ -56,7 +58,12 @@ def unpack_records(plies):
 
 def gather_records(records, dst=0, group=None):
     """Gather every rank's finished games to `dst` (torch.distributed, any backend).
-    Returns the merged records sorted by game id on dst, None elsewhere."""
+    Returns the merged records sorted by game id on dst, None elsewhere.
+
+    Only dst receives: the ranks exchange their byte counts (one 8-byte all-gather), then
+    every other rank sends its packed plies point-to-point to dst (RCCL send/recv over
+    xGMI, or gloo on the CPU), which receives each into a buffer of exactly that size.
+    No rank but dst allocates more than its own records."""
     import torch
     import torch.distributed as dist
 
@@ -69,15 +76,18 @@ def gather_records(records, dst=0, group=None):
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     sizes = [int(s.item()) for s in sizes]
-    cap = max(sizes) if sizes else 0
-    buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    if local.size:
-        buf[:local.size] = torch.from_numpy(local).to(dev)
-    bufs = [torch.zeros(cap, dtype=torch.uint8, device=dev) for _ in range(world)]
-    dist.all_gather(bufs, buf, group=group)  # one fixed-size exchange (nccl has no variable gather)
+    glob = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)  # noqa: E731
     if rank != dst:
+        if local.size:
+            dist.send(torch.from_numpy(local).to(dev), glob(dst), group=group)
         return None
-    parts = [b[:s].cpu().numpy().view(PLY_DTYPE) for b, s in zip(bufs, sizes)]
+    parts = [local.view(PLY_DTYPE)]
+    for r in range(world):
+        if r == rank or sizes[r] == 0:
+            continue
+        buf = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
+        dist.recv(buf, glob(r), group=group)
+        parts.append(buf.cpu().numpy().view(PLY_DTYPE))
     return unpack_records(np.concatenate(parts) if parts else np.zeros(0, PLY_DTYPE))
 
 
@@ -117,7 +127,10 @@ def init_from_env():
         local = local % torch.cuda.device_count()  # more ranks than GPUs: ranks share them
         torch.cuda.set_device(local)
     if not dist.is_initialized():
-        backend = os.environ.get("UTTT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        # RCCL refuses two ranks on one device: ranks sharing GPUs use gloo
+        shared = torch.cuda.is_available() and world > torch.cuda.device_count()
+        backend = os.environ.get("UTTT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() and not shared
+                                                          else "gloo")
         dist.init_process_group(backend)
     return dist.get_rank(), dist.get_world_size(), local
 
@@ -134,7 +147,7 @@ def broadcast_int(value, src=0):
 
 
 def self_play_sharded(model, n_games, slots, seed_base, evaluate_count=50, batch_size=8, temperature=1.0,
-                      lanes=None, progress=None, evaluator_kind=None):
+                      lanes=None, progress=None, evaluator_kind=None, timings=None):
     """Run this rank's contiguous shard of game ids [0, n_games) and gather every rank's records to
     rank 0 (records with inputs on rank 0, None elsewhere). Game g plays from RandomState(seed_base + g)
     whatever the world size, so the gathered records equal a single-GPU run."""
@@ -153,7 +166,15 @@ def self_play_sharded(model, n_games, slots, seed_base, evaluate_count=50, batch
         dev = torch.cuda.current_device() if torch.cuda.is_available() else None
         sp = SelfPlay(n_slots, evaluate_count, batch_size, temperature, device=dev, model=model, lanes=n_lanes,
                       evaluator_kind=evaluator_kind)
-        sp.run(b, e, seed_base, progress)
+        t = sp.run(b, e, seed_base, progress)
+        if timings is not None:
+            timings["games_s"] = t
+            timings["sims"] = sp.sims
         recs = sp.records(with_inputs=False)
+    t0 = time.perf_counter()
     out = gather_records(recs)
-    return records_to_inputs(out) if out is not None else None
+    t1 = time.perf_counter()
+    out = records_to_inputs(out) if out is not None else None
+    if timings is not None:
+        timings.update(gather_s=t1 - t0, inputs_s=time.perf_counter() - t1)
+    return out

@@ -206,9 +206,10 @@ class Engine:
         check(self.lib.uttt_engine_cache_clear(self.h))
 
     def cache_stats(self):
-        h, m, i = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        check(self.lib.uttt_engine_cache_stats(self.h, ctypes.byref(h), ctypes.byref(m), ctypes.byref(i)))
-        return {"hits": h.value, "misses": m.value, "inserts": i.value}
+        h, m, i, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.uttt_engine_cache_stats2(self.h, ctypes.byref(h), ctypes.byref(m), ctypes.byref(i),
+                                                ctypes.byref(r)))
+        return {"hits": h.value, "misses": m.value, "inserts": i.value, "replacements": r.value}
 
     # ------------------------------------------------------------- telemetry --
     def set_timing(self, on=True):

@@ -158,9 +158,11 @@ class SelfPlay:
     # one evaluator object per lane (each owns its buffers); with one lane the
     # attribute form is kept for compatibility
     def set_evaluator(self, make):
-        """make(engine) -> evaluator, called once per lane."""
+        """make(engine) -> evaluator, called once per lane. A new evaluator may compute other
+        values: the shared evaluation table is cleared (its owner is lane 0)."""
         for ln in self.lanes:
             ln.evaluator = make(ln.engine)
+        self.lanes[0].engine.cache_clear()
 
     @property
     def evaluator(self):
@@ -246,7 +248,7 @@ class SelfPlay:
         return out
 
     def cache_stats(self):
-        out = {"hits": 0, "misses": 0, "inserts": 0}
+        out = {"hits": 0, "misses": 0, "inserts": 0, "replacements": 0}
         for ln in self.lanes:
             st = ln.engine.cache_stats()
             for k in out:

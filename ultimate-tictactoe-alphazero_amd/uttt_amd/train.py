@@ -90,14 +90,85 @@ def local_slice(idx, rank, world):
     return idx[b:b + base + (1 if rank < extra else 0)]
 
 
+class GraphedStep:
+    """One optimiser step of the static global batch (gather from the resident dataset, forward,
+    loss, backward, Adam) captured once in a HIP graph and replayed per batch: ~300 kernels per
+    step become one graph launch, so the step is no longer bound by host launch overhead.
+
+    Adam runs with capturable=True and a device-tensor learning rate (the epoch's LambdaLR factor
+    is written into it, not baked into the graph). The warm-up steps the capture needs are undone
+    (parameters, buffers and optimiser state restored in place), so training starts from the
+    caller's weights exactly as the eager loop does. The graph adds the step's loss to a device
+    accumulator; batches of another size (an epoch's last) run the same body eagerly."""
+
+    def __init__(self, model, opt, x, p, v, batch_size, channels_last=False):
+        self.model, self.opt, self.x, self.p, self.v = model, opt, x, p, v
+        self.channels_last = channels_last
+        dev = x.device
+        self.idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
+        self.loss_sum = torch.zeros((), device=dev)
+        snap = {k: t.detach().clone() for k, t in model.state_dict().items()}
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):  # allocator, MIOpen kernel choice, optimiser state
+                opt.zero_grad(set_to_none=True)
+                self._body(self.idx)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self._body(self.idx)
+        # undo the warm-up: the same tensors (the graph's addresses), the caller's values
+        with torch.no_grad():
+            for k, t in model.state_dict().items():
+                t.copy_(snap[k])
+            for st in opt.state.values():
+                for name, t in st.items():
+                    if torch.is_tensor(t):
+                        t.zero_()
+        self.loss_sum.zero_()
+
+    def _body(self, idx):
+        xb = self.x.index_select(0, idx)
+        if self.channels_last:
+            xb = xb.contiguous(memory_format=torch.channels_last)
+        pred_p, pred_v = self.model(xb)
+        loss = policy_loss_fn(pred_p, self.p.index_select(0, idx)) + \
+            nn.functional.mse_loss(pred_v, self.v.index_select(0, idx))
+        loss.backward()
+        self.opt.step()
+        self.loss_sum += loss.detach()
+        return loss
+
+    def step(self, idx):
+        if idx.numel() == self.idx.numel():
+            self.idx.copy_(idx, non_blocking=True)
+            self.graph.replay()
+        else:
+            self.opt.zero_grad(set_to_none=False)
+            self._body(idx)
+
+
+def _use_graph(graph, device, world):
+    if graph is None:
+        import os
+        graph = os.environ.get("UTTT_TRAIN_GRAPH", "1") != "0"
+    return bool(graph) and world == 1 and device.type == "cuda"
+
+
 def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, device=None, seed=0, lr=0.001,
-                  log=print, sync_bn=None):
+                  log=print, sync_bn=None, graph=None, channels_last=False):
     """Train `model` (a DualNetwork) on `history` in place; returns the per-epoch mean losses.
-    In a torch.distributed job every rank calls this with the same history and seed."""
+    In a torch.distributed job every rank calls this with the same history and seed.
+    graph (default on for one GPU; UTTT_TRAIN_GRAPH=0 disables): replay the step as a HIP graph
+    (GraphedStep); the eager loop otherwise (and for the data-parallel path)."""
     rank, world = _world()
     device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
                         else torch.device("cpu"))
     x, p, v = (torch.from_numpy(a).to(device) for a in history_arrays(history))  # resident in HBM
+    if _use_graph(graph, device, world):
+        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last)
     net = prepare(model, device, sync_bn)
     opt = torch.optim.Adam(net.parameters(), lr=lr)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lr_lambda=lr_lambda)
@@ -121,5 +192,31 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
     return losses
 
 
-__all__ = ["BATCH_SIZE", "RN_EPOCHS", "batches", "history_arrays", "local_slice", "lr_lambda", "policy_loss_fn",
-           "prepare", "train_network", "train_step"]
+def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last):
+    net = model.to(device)
+    if channels_last:
+        net = net.to(memory_format=torch.channels_last)
+    net.train()
+    lr_t = torch.tensor(lr, dtype=torch.float32, device=device)
+    opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, foreach=True)
+    step = GraphedStep(net, opt, x, p, v, batch_size, channels_last)
+    losses = []
+    for epoch in range(epochs):
+        lr_t.fill_(lr * lr_lambda(epoch))
+        step.loss_sum.zero_()
+        idxs = batches(len(x), batch_size, epoch, seed)
+        perm = torch.cat(idxs).to(device, non_blocking=True)
+        o = 0
+        for b in idxs:
+            step.step(perm[o:o + len(b)])
+            o += len(b)
+        losses.append(float(step.loss_sum) / len(idxs))
+        if log:
+            log(f"Epoch {epoch + 1}/{epochs}, Loss: {losses[-1]:.4f}, LR: {lr * lr_lambda(epoch + 1):.6f}")
+    if channels_last:
+        net.to(memory_format=torch.contiguous_format)
+    return losses
+
+
+__all__ = ["BATCH_SIZE", "GraphedStep", "RN_EPOCHS", "batches", "history_arrays", "local_slice", "lr_lambda",
+           "policy_loss_fn", "prepare", "train_network", "train_step"]
