@@ -33,7 +33,8 @@ def timeit(fn, reps=30):
 
 def main():
     lib = _lib.load()
-    lib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
+    dlib = _lib.load_diag()
+    dlib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
         [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
     net = random_network(0)
     w, b = fold_bn(net.residual_blocks[8].conv1, net.residual_blocks[8].bn1)
@@ -48,7 +49,7 @@ def main():
         ba = board_amax(x)
         # residual-form modes (bit 20) read a separate tensor, as the tower's block input is
         r = torch.relu(torch.randn(n, 81, 128, device="cuda", generator=g))
-        lib.uttt_diag_wino3h_set_residual(_p(r))
+        dlib.uttt_diag_wino3h_set_residual(_p(r))
         y0 = torch.empty_like(x)
         t_prod = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), None, _p(y0),
                                                           _p(ba), 1, None, None, 0, n, st))
@@ -57,7 +58,7 @@ def main():
             y = torch.full_like(x, float("nan"))
             # the ablation launch takes one max for every board: pass the product's per-board row
             # through a per-board launch is not available there, so use a uniform bound
-            t = timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(u8 if m & (256 | 8192) else uh),
+            t = timeit(lambda m=m: dlib.uttt_diag_wino3h_ablation(_p(x), _p(u8 if m & (256 | 8192) else uh),
                                                                   ctypes.c_float(su), _p(b), _p(y),
                                                                   _p(ba.max().reshape(1)), n, m, st))
             ent = {"us": round(t, 1), "tflops_exec": round(22118400 * n / t / 1e6, 1)}

@@ -15,7 +15,8 @@ from uttt_amd.model import fold_bn, random_network  # noqa: E402
 from uttt_amd.nnfast import amax, wino3h_weights, _p  # noqa: E402
 
 lib = _lib.load()
-lib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
+    dlib = _lib.load_diag()
+dlib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
     [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
 net = random_network(0)
 w, b = fold_bn(net.residual_blocks[8].conv1, net.residual_blocks[8].bn1)
@@ -28,10 +29,10 @@ for n, mode in [(int(a), m) for a in (sys.argv[1:] or ["1344"]) for m in MODES]:
     y = torch.empty_like(x)
     xa = amax(x)
     for _ in range(5):
-        lib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y), _p(xa), n, mode, st)
+        dlib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y), _p(xa), n, mode, st)
     torch.cuda.synchronize()
     ph = np.zeros((64, 2, 8, 6), np.uint32)
-    assert lib.uttt_diag_wino3h_stamps(ph.ctypes.data_as(ctypes.c_void_p)) == 0
+    assert dlib.uttt_diag_wino3h_stamps(ph.ctypes.data_as(ctypes.c_void_p)) == 0
     med = np.median(ph.astype(np.float64), axis=0)
     print(f"boards {n} mode {mode}: phase cycles (median over 64 WGs), cumulative -> deltas")
     names = ["load_x", "transform", "barrier+store_x", "gemm", "epilogue", "barrier"]

@@ -31,7 +31,8 @@ def timeit(fn, reps=20):
 
 def main():
     lib = _lib.load()
-    lib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
+    dlib = _lib.load_diag()
+    dlib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
         [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
     net = random_network(0)
     w, b = fold_bn(net.residual_blocks[8].conv1, net.residual_blocks[8].bn1)
@@ -49,11 +50,11 @@ def main():
         r = torch.randn_like(x)
         th_res = timeit(lambda: lib.uttt_nn_conv3x3_wino3h(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(r), _p(y),
                                                           _p(ba), 1, None, None, 0, n, st))
-        abl = {m: timeit(lambda m=m: lib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y),
+        abl = {m: timeit(lambda m=m: dlib.uttt_diag_wino3h_ablation(_p(x), _p(uh), ctypes.c_float(su), _p(b), _p(y),
                                                                     _p(xa), n, m, st)) for m in [int(v) for v in os.environ.get("MODES", "1,2,8,64,16,32,48,49,112,512").split(",")]}
-        lib.uttt_diag_wino3h_pf.argtypes = lib.uttt_diag_wino3h_ablation.argtypes
+        dlib.uttt_diag_wino3h_pf.argtypes = dlib.uttt_diag_wino3h_ablation.argtypes
         for pf in [int(v) for v in os.environ.get("PFS", "").split(",") if v]:
-            abl["pf%d" % pf] = timeit(lambda pf=pf: lib.uttt_diag_wino3h_pf(_p(x), _p(uh), ctypes.c_float(su), _p(b),
+            abl["pf%d" % pf] = timeit(lambda pf=pf: dlib.uttt_diag_wino3h_pf(_p(x), _p(uh), ctypes.c_float(su), _p(b),
                                                                             _p(y), _p(xa), n, pf, st))
         xs = x[:min(n, 512)]
         ref = F.conv2d(xs.reshape(-1, 9, 9, 128).permute(0, 3, 1, 2).double(), wc.double(), b.double(), padding=1)
@@ -62,7 +63,7 @@ def main():
         torch.cuda.synchronize()
         sc = ref.abs().max().item()
         u8 = uh.repeat(8)
-        abl[256] = timeit(lambda: lib.uttt_diag_wino3h_ablation(_p(x), _p(u8), ctypes.c_float(su), _p(b), _p(y),
+        abl[256] = timeit(lambda: dlib.uttt_diag_wino3h_ablation(_p(x), _p(u8), ctypes.c_float(su), _p(b), _p(y),
                                                                 _p(xa), n, 256, st))
         rec = {"boards": n, "wino3h_us": round(th, 1), "wino3h_res_us": round(th_res, 1), "ablation_us": {str(k): round(v, 1) for k, v in abl.items()},
                "direct_equiv_tflops": round(2 * 81 * 128 * 1152 * n / th / 1e6, 1),

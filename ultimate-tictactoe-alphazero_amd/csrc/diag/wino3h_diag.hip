@@ -1,0 +1,125 @@
+// wino3h_diag.hip — diagnostics-only instantiations of k_wino3h_conv (timing ablations, phase
+// stamps, prefetch-distance variants) in their own library, libuttt_diag.so (Makefile target
+// `diag`, used by tools/diag/*.py). Nothing in the product library or its tests loads it.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "uttt_nn.h"
+#include "wino3h_impl.h"
+
+using namespace uttt;
+
+// diagnostic: the residual form of an ablation launch (residual = g_diag_res if set, else x)
+static const float *g_diag_res = nullptr;
+template <int MODE>
+static void ablation_res(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
+                         const uint32_t *x_amax, int32_t n_boards, hipStream_t st) {
+    using namespace wino3h;
+    hipLaunchKernelGGL((k_wino3h_conv<true, MODE>), dim3(grid_size(n_boards)), dim3(NT), 0, st, x, u, u_scale, bias,
+                       g_diag_res ? g_diag_res : x, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+}
+
+extern "C" {
+
+// Diagnostic: the residual tensor of the ablation's residual form (null: x itself)
+void uttt_diag_wino3h_set_residual(const float *res) { g_diag_res = res; }
+
+// Diagnostic (not declared in uttt_nn.h): the same launch with a timing ablation.
+int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
+                              const uint32_t *x_amax, int32_t n_boards, int32_t mode, void *stream) {
+    const dim3 grid(wino3h::grid_size(n_boards));
+    hipStream_t st = (hipStream_t)stream;
+    using namespace wino3h;
+    if (mode & (1 << 20)) {  // the residual form (residual = x)
+        switch (mode & ~(1 << 20)) {
+            case 65536: ablation_res<65536>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case 131072: ablation_res<131072>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case 196608: ablation_res<196608>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case 8: ablation_res<8>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            default: ablation_res<0>(x, u, u_scale, bias, y, x_amax, n_boards, st);
+        }
+        return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+    }
+    switch (mode) {
+        case 131072: hipLaunchKernelGGL((k_wino3h_conv<false, 131072>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 16: hipLaunchKernelGGL((k_wino3h_conv<false, 16>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 32: hipLaunchKernelGGL((k_wino3h_conv<false, 32>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 48: hipLaunchKernelGGL((k_wino3h_conv<false, 48>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 68: hipLaunchKernelGGL((k_wino3h_conv<false, 68>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 116: hipLaunchKernelGGL((k_wino3h_conv<false, 116>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 20: hipLaunchKernelGGL((k_wino3h_conv<false, 20>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 8192: hipLaunchKernelGGL((k_wino3h_conv<false, 8192>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 8196: hipLaunchKernelGGL((k_wino3h_conv<false, 8196>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 260: hipLaunchKernelGGL((k_wino3h_conv<false, 260>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+    }
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+// Diagnostic: MODE-4 phase stamps, out[64][2][8][6] (see g_stamp).
+int uttt_diag_wino3h_stamps(unsigned int *out) {
+    if (!out || hipMemcpyFromSymbol(out, HIP_SYMBOL(wino3h::g_stamp), sizeof(unsigned int) * 64 * 2 * 8 * 6) != hipSuccess)
+        return UTTT_ERR_HIP;
+    return UTTT_OK;
+}
+
+// Diagnostic: pipeline variants, product arithmetic (same output bits as the product launch):
+// variant 0 product, 1 buffer-loaded inputs, 2 no V lookahead + U PF 4, 3 no V lookahead + PF 5,
+// 4 = 1 + 2, 5 = 1 + 3; residual form when res is non-null.
+int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *res,
+                             float *y, const uint32_t *x_amax, int32_t n_boards, int32_t variant, void *stream) {
+    const dim3 grid(wino3h::grid_size(n_boards));
+    hipStream_t st = (hipStream_t)stream;
+    using namespace wino3h;
+#define UTTT_V(M, P)                                                                                                  \
+    do {                                                                                                              \
+        if (res)                                                                                                      \
+            hipLaunchKernelGGL((k_wino3h_conv<true, M, P>), grid, dim3(NT), 0, st, x, u, u_scale, bias, res, y, x_amax, \
+                               1, nullptr, nullptr, 0, n_boards);                                                    \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_wino3h_conv<false, M, P>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y,   \
+                               x_amax, 1, nullptr, nullptr, 0, n_boards);                                            \
+    } while (0)
+    switch (variant) {
+        case 1: UTTT_V(kBufferX, 3); break;
+        case 2: UTTT_V(kNoALookahead, 4); break;
+        case 3: UTTT_V(kNoALookahead, 5); break;
+        case 4: UTTT_V(kBufferX | kNoALookahead, 4); break;
+        case 5: UTTT_V(kBufferX | kNoALookahead, 5); break;
+        case 6: UTTT_V(kNoALookahead, 3); break;
+        default: UTTT_V(0, 3);
+    }
+#undef UTTT_V
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+int uttt_diag_wino3h_pf(const float *x, const uint16_t *u, float u_scale, const float *bias, float *y,
+                        const uint32_t *x_amax, int32_t n_boards, int32_t pf, void *stream) {
+    const dim3 grid(wino3h::grid_size(n_boards));
+    hipStream_t st = (hipStream_t)stream;
+    using namespace wino3h;
+    switch (pf) {
+        case 3: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 6: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 6>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+    }
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+}  // extern "C"

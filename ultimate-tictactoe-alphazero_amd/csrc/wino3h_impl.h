@@ -1,0 +1,635 @@
+// wino3h_impl.h — k_wino3h_conv, the split-f16 Winograd F(3x3,3x3) tower conv, as a template
+// shared by the product library (csrc/wino3h_conv.hip: MODE 0 only) and the diagnostics library
+// (csrc/diag/wino3h_diag.hip: timing ablations, phase stamps, prefetch variants). MODE bits are
+// `if constexpr` branches: MODE 0 compiles none of them. Algorithm and layout: wino3h_conv.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "uttt_nn.h"
+
+namespace uttt {
+
+namespace wino3h {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int C = 128;        // channels in and out
+constexpr int NP = 25;        // transform points
+constexpr int KC = 32;        // input channels per chunk (one K=32 MFMA step)
+constexpr int NCH = C / KC;   // chunks per set
+constexpr int GB = 7;         // boards per group: its 63 tiles are two sets of 32 tile slots
+constexpr int TS = 32;        // tile slots per set (two 16-tile MFMA blocks; the group's 64th is empty)
+constexpr int SB = 4;         // boards a set's tiles touch: boards 0-3 or 3-6 of its group
+constexpr int SR = 10;        // staged row stride: one zero column (shared by neighbouring rows) + 9 cells
+constexpr int XP = (SB * 10 + 1) * SR + 1;  // staged positions (411): boards stacked under shared zero rows
+constexpr int NT = 512;       // threads (8 waves)
+constexpr int NITEM = TS * (KC / 2);             // transform items per chunk (tile slot, channel pair): 512
+constexpr int VPLANE = 1024;                     // bytes of one (xi, rt, hi|lo) A plane: 4 kq x 16 rows x 16 B
+constexpr int VB = NP * 4 * VPLANE;              // V bytes: [xi][rt][h][kq][row^2kq][8 f16]
+constexpr int XF4 = SB * 81 * (KC / 4);          // float4s staged per chunk (2592)
+constexpr int XPT = (XF4 + NT - 1) / NT;         // per thread (6)
+static_assert(NITEM == NT, "one transform item per thread");
+constexpr int NPAD = XP - SB * 81;  // zero positions of the staged layout (87)
+static_assert(NPAD == 5 * 10 + 4 * 9 + 1, "pad positions: shared zero rows, zero column, last position");
+static_assert(XP * KC * 4 + VB <= 160 * 1024, "LDS");
+
+// Sets of n boards: two per full group of 7, one or two for a partial last group
+// (the first set of a group covers boards 0-2 and 5 tiles of board 3).
+__host__ __device__ constexpr int n_sets(int n) { return 2 * (n / GB) + (n % GB == 0 ? 0 : (n % GB <= 3 ? 1 : 2)); }
+// Staged position of cell (r, c) of staged board k; r or c = -1 / 9 land on zero pads.
+__host__ __device__ constexpr int spos(int k, int r, int c) { return (10 * k + r + 1) * SR + c + 1; }
+
+// Toom-Cook F(3,3) on {0, 1, -1, 2, inf} (as wino3_conv.hip)
+__host__ __device__ constexpr int at(int a, int u) {
+    constexpr int m[3][5] = {{1, 1, 1, 1, 0}, {0, 1, -1, 2, 0}, {0, 1, 1, 4, 1}};
+    return m[a][u];
+}
+
+struct Acc {
+    floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
+};
+
+// fold of point P, as single packed ops o = (row a with A^T[a][u] != 0, pair j),
+// spread over the next point's six MFMA slots
+__host__ __device__ constexpr int n_rows(int u) { return (at(0, u) != 0) + (at(1, u) != 0) + (at(2, u) != 0); }
+__host__ __device__ constexpr int nth_row(int u, int i) {
+    int a = 0;
+    for (; a < 3; ++a)
+        if (at(a, u) != 0 && i-- == 0) break;
+    return a;
+}
+
+// Points whose A^T column has one nonzero (u = 0 -> row 0, u = 4 -> row 2, both coefficient 1)
+// accumulate straight into their S row as the MFMA's C operand: no fold ops for 10 of the 25
+// points (40 of 220 packed adds per chunk; 2-10% per launch, round 2)
+template <int P, int MODE>
+__host__ __device__ constexpr bool acc_direct() { return n_rows(P / 5) == 1; }
+
+template <int P, int O, int MODE>
+__device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    constexpr int u = P / 5, v = P % 5;
+    if constexpr (O < 4 * n_rows(u) && !acc_direct<P, MODE>()) {
+        constexpr int a = nth_row(u, O / 4), j = O % 4, K = at(a, u);
+        // Inline asm is outside the compiler's hazard recognizer, so nothing pads these reads of
+        // the previous point's MFMA results; the schedule keeps >= 6 instructions, one of them an
+        // MFMA, between producer and reader, and the output bits equal those of a compiler-visible
+        // fold (builtin packed ops, hazard-padded; 7% slower from spills) on the same inputs
+        // (round 2, tools/diag/wino3h_modes.py).
+        if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        else if constexpr (K == -1)
+            asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        else if constexpr (K == 2) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k2));
+        else asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k4));
+    }
+}
+
+constexpr int NSLOT = 6;  // MFMAs per point
+template <int P, int SL, int MODE, int O = 0>
+__device__ __forceinline__ void fold_slot(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    constexpr int nops = 4 * n_rows(P / 5);
+    if constexpr (O < nops) {
+        if constexpr (O * NSLOT / nops == SL) fold_op<P, O, MODE>(S, m, k2, k4);
+        fold_slot<P, SL, MODE, O + 1>(S, m, k2, k4);
+    }
+}
+
+template <int P, int MODE>
+__device__ __forceinline__ void fold_all(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
+    fold_slot<P, 0, MODE>(S, m, k2, k4);
+    fold_slot<P, 1, MODE>(S, m, k2, k4);
+    fold_slot<P, 2, MODE>(S, m, k2, k4);
+    fold_slot<P, 3, MODE>(S, m, k2, k4);
+    fold_slot<P, 4, MODE>(S, m, k2, k4);
+    fold_slot<P, 5, MODE>(S, m, k2, k4);
+}
+
+// U fragments (hi, lo) of one point: U[xi][chunk][h][co/16][kq][co%16][8 f16]; each of the
+// two loads reads 1 KB contiguous and lane-linear per wave (hi and lo planes 8 KB apart)
+struct BFrag {
+    halfx8 h, l;
+};
+constexpr int UPLANE = C * 4 * 16;  // bytes of one (xi, chunk, hi|lo) plane
+__device__ __forceinline__ BFrag load_b(rsrc_t u, int xi, int chunk, int voff) {
+    const int soff = (xi * NCH + chunk) * 2 * UPLANE;
+    BFrag b;
+    b.h = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff, soff, 0));
+    b.l = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff + UPLANE, soff, 0));
+    return b;
+}
+template <int XI>
+__device__ __forceinline__ BFrag load_b_ahead(rsrc_t u, int chunk, int voff) {
+    if constexpr (XI < NP) return load_b(u, XI, chunk, voff);
+    else return load_b(u, XI - NP, (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
+}
+
+// A fragments (V hi / lo of both row blocks) of one point
+struct AFrag {
+    halfx8 h0, l0, h1, l1;
+};
+__device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
+    // sv already points at this lane's 16-byte slot within a plane
+    const char *p = sv + xi * 4 * VPLANE;
+    AFrag a;
+    a.h0 = *reinterpret_cast<const halfx8 *>(p);
+    a.l0 = *reinterpret_cast<const halfx8 *>(p + VPLANE);
+    a.h1 = *reinterpret_cast<const halfx8 *>(p + 2 * VPLANE);
+    a.l1 = *reinterpret_cast<const halfx8 *>(p + 3 * VPLANE);
+    return a;
+}
+
+// Variant bits (diagnostic builds; the product is MODE 0)
+constexpr int kNoALookahead = 1 << 21;  // V fragments read at their own point (frees 16 VGPRs for U prefetch)
+constexpr int kBufferX = 1 << 22;       // input loads as buffer loads, zero beyond the batch: no branches
+
+// Point loop, software-pipelined: B PF points ahead (L2), A one point ahead (LDS).
+// The fold of point XI-1 is issued among point XI's MFMAs.
+template <int XI, int MODE, int PF>
+__device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag (&bq)[PF],
+                                        AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff) {
+    if constexpr (XI <= NP) {
+        floatx2 m[4];
+        if constexpr (XI < NP) {
+            BFrag b2;
+            if constexpr (MODE & 32) {  // diagnostic: no B loads (operands reused, laundered)
+                b2 = bq[0];
+                asm volatile("" : "+v"(b2.h), "+v"(b2.l));
+            } else {
+                b2 = load_b_ahead<XI + PF>(u, chunk, voff);
+            }
+            const BFrag b0 = bq[0];
+            if constexpr (MODE & kNoALookahead) a0 = load_a(sv, XI);  // this point's V, waited for here
+            AFrag a1;
+            if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) {
+                if constexpr (MODE & 16) {  // diagnostic: no A loads
+                    a1 = a0;
+                    asm volatile("" : "+v"(a1.h0), "+v"(a1.l0), "+v"(a1.h1), "+v"(a1.l1));
+                } else {
+                    a1 = load_a(sv, XI + 1);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            floatx4 m0 = {}, m1 = {};
+            constexpr int srow = nth_row(XI / 5, 0) * 5 + XI % 5;  // the S row of a direct point
+            if constexpr (acc_direct<XI, MODE>()) {
+                m0 = floatx4{S[srow].p[0].x, S[srow].p[0].y, S[srow].p[1].x, S[srow].p[1].y};
+                m1 = floatx4{S[srow].p[2].x, S[srow].p[2].y, S[srow].p[3].x, S[srow].p[3].y};
+            }
+            constexpr bool fold_here = XI > 0 && !(MODE & 64);
+            // small terms first, then the hi x hi product
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h0, m0, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 0, MODE>(S, mprev, k2, k4);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h1, m1, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 1, MODE>(S, mprev, k2, k4);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l0, m0, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 2, MODE>(S, mprev, k2, k4);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l1, m1, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 3, MODE>(S, mprev, k2, k4);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h0, m0, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 4, MODE>(S, mprev, k2, k4);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
+            if constexpr (fold_here) fold_slot<XI - 1, 5, MODE>(S, mprev, k2, k4);
+            asm volatile("" : "+v"(m0), "+v"(m1));  // keep this point's MFMAs in its own region
+            if constexpr (acc_direct<XI, MODE>()) {
+                S[srow].p[0] = __builtin_shufflevector(m0, m0, 0, 1);
+                S[srow].p[1] = __builtin_shufflevector(m0, m0, 2, 3);
+                S[srow].p[2] = __builtin_shufflevector(m1, m1, 0, 1);
+                S[srow].p[3] = __builtin_shufflevector(m1, m1, 2, 3);
+            }
+            m[0] = __builtin_shufflevector(m0, m0, 0, 1);
+            m[1] = __builtin_shufflevector(m0, m0, 2, 3);
+            m[2] = __builtin_shufflevector(m1, m1, 0, 1);
+            m[3] = __builtin_shufflevector(m1, m1, 2, 3);
+#pragma unroll
+            for (int i = 0; i + 1 < PF; ++i) bq[i] = bq[i + 1];
+            bq[PF - 1] = b2;
+            if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) a0 = a1;
+        }
+        if constexpr (XI == NP && !(MODE & 64)) fold_all<XI - 1, MODE>(S, mprev, k2, k4);  // nothing left to spread it over
+        if constexpr (XI < NP) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mprev[i] = m[i];
+            xi_loop<XI + 1, MODE, PF>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff);
+        }
+    }
+}
+
+// inputs of chunk `chunk` of the set starting at board b0 -> registers
+template <int MODE>
+__device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restrict__ x, int b0, int n_boards, int chunk,
+                                       int tid) {
+    // the staged boards are consecutive: their positions are one run of rows of x
+    const int rows = (n_boards - b0) * 81;
+    if constexpr (MODE & kBufferX) {
+        // one resource per set whose range ends at the batch's last board: loads past it return 0,
+        // so no lane branches and the compiler counts the loads exactly (precise vmcnt waits)
+        const int nb = min(rows, SB * 81);
+        const rsrc_t xr_ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(x + (size_t)b0 * 81 * C), 0,
+                                                             nb * C * 4, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < XPT; ++k) {
+            const int i = tid + k * NT;
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const int off = i < XF4 ? (bp * C + chunk * KC + 4 * q) * 4 : 0x7ffffff0;
+            const floatx4 t = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr_, off, 0, 2));
+            xr[k] = make_float4(t.x, t.y, t.z, t.w);
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+        const int i = tid + k * NT;
+        xr[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (i < XF4) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            if (bp < rows) {
+                const float4 *src = reinterpret_cast<const float4 *>(x + ((size_t)b0 * 81 + bp) * C + chunk * KC) + q;
+                if constexpr (!(MODE & 512)) {
+                    const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4 *>(src));
+                    xr[k] = make_float4(t.x, t.y, t.z, t.w);
+                }
+                else xr[k] = *src;
+            }
+        }
+    }
+}
+
+// Per-board V scales of the SB staged boards of a set (powers of two, uniform over the workgroup)
+struct SetScale {
+    float s[SB];
+    __device__ __forceinline__ float of(int kb) const {
+        // a select chain, not a dynamically indexed array (that would live in scratch)
+        return kb == 0 ? s[0] : (kb == 1 ? s[1] : (kb == 2 ? s[2] : s[3]));
+    }
+};
+
+// registers -> sX[padded position][32 channels], scaled by its board's sv (a power of two: exact)
+__device__ __forceinline__ void store_x(float *__restrict__ sX, const float4 (&xr)[XPT], const SetScale &sc, int tid) {
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+        const int i = tid + k * NT;
+        if (i < XF4) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const int kb = bp / 81, pos = bp - 81 * kb, sp = spos(kb, pos / 9, pos % 9);
+            const float sv = sc.of(kb);
+            float4 v = xr[k];
+            v.x *= sv;
+            v.y *= sv;
+            v.z *= sv;
+            v.w *= sv;
+            reinterpret_cast<float4 *>(sX + sp * KC)[q] = v;
+        }
+    }
+}
+
+// x -> B^T x for one 5-vector (channel pairs), common subexpressions shared
+__device__ __forceinline__ void bt5(const floatx2 (&d)[5], floatx2 (&t)[5]) {
+    const floatx2 two = {2.0f, 2.0f}, mtwo = {-2.0f, -2.0f};
+    const floatx2 e = d[3] - d[2];
+    const floatx2 f = d[1] - d[2];
+    const floatx2 t3 = d[3] - d[1];
+    const floatx2 g = d[0] - d[2];
+    const floatx2 h = d[4] - d[2];
+    t[0] = __builtin_elementwise_fma(two, g, t3);
+    t[1] = __builtin_elementwise_fma(mtwo, d[1], e);
+    t[2] = __builtin_elementwise_fma(two, f, e);
+    t[3] = t3;
+    t[4] = __builtin_elementwise_fma(mtwo, t3, h);
+}
+
+// (v0, v1) -> packed f16 hi (round to nearest: |v - hi| <= 2^-11 |v|, exact in f32) and
+// f16 lo = the remainder rounded to nearest (v_cvt_pk_f16_f32, one instruction each)
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split(floatx2 v, uint32_t &hi, uint32_t &lo) {
+    const halfx2 h = __builtin_convertvector(v, halfx2);
+    const floatx2 r = v - __builtin_convertvector(h, floatx2);
+    const halfx2 l = __builtin_convertvector(r, halfx2);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// V = B^T d B for item it = (tile slot lt, channel pair p) of a set that is half h of its
+// group -> split -> sV in fragment order, in two halves: transform_rows (u = d B; reads sX
+// only) and transform_cols (V = B^T u, split, LDS stores into sV). Slot 31 of the second half has no tile: it repeats tile 62, whose
+// results the epilogue drops.
+__device__ __forceinline__ void transform_rows(floatx2 (&uu)[5][5], const float *__restrict__ sX, int it, int h) {
+    const int p = it % (KC / 2), lt = it / (KC / 2);
+    const int gt = min(32 * h + lt, GB * 9 - 1), gb = gt / 9, tt = gt - 9 * gb, ty = tt / 3, tx = tt % 3;
+    const float *xs = sX + spos(gb - 3 * h, 3 * ty - 1, 3 * tx - 1) * KC + 2 * p;
+    // one row of d live at a time (loads one row ahead; fenced so the scheduler does not
+    // hoist all 25 of them next to the fifteen live accumulators)
+    floatx2 d[2][5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) d[0][j] = *reinterpret_cast<const floatx2 *>(xs + j * KC);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        if (i < 4) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[(i + 1) & 1][j] = *reinterpret_cast<const floatx2 *>(xs + ((i + 1) * SR + j) * KC);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bt5(d[i & 1], uu[i]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floatx2 (&uu)[5][5], int it) {
+    const int p = it % (KC / 2), lt = it / (KC / 2);
+    // A fragment: lane (row m, kq) holds k = 8kq..8kq+7; channel pair p is k = 2p, 2p+1
+    const int rt = lt >> 4, m = lt & 15, kq = p >> 2, w = p & 3;
+    char *base = sv + rt * 2 * VPLANE + kq * 256 + ((m ^ (2 * kq)) * 16) + 4 * w;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        const floatx2 col[5] = {uu[0][b], uu[1][b], uu[2][b], uu[3][b], uu[4][b]};
+        floatx2 o[5];
+        bt5(col, o);
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+            uint32_t hi, lo;
+            split(o[a], hi, lo);
+            char *q = base + (a * 5 + b) * 4 * VPLANE;
+            *reinterpret_cast<uint32_t *>(q) = hi;
+            *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;
+        }
+    }
+}
+
+__device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it, int h) {
+    floatx2 uu[5][5];
+    transform_rows(uu, sX, it, h);
+    transform_cols(sv, uu, it);
+}
+
+// An opaque copy: index math derived from it is recomputed where it is used
+// instead of being hoisted out of the chunk loop into (spilled) registers.
+__device__ __forceinline__ int fresh(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// Workgroup barrier for the LDS hand-offs only: unlike __syncthreads() it does not wait
+// for outstanding global loads (the next chunk's inputs) or stores (the epilogue).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ float pow2_scale(float amax) {
+    // largest power of two s with 36 * amax * s <= 2^15 (1 for 0 / non-finite)
+    const float b = 36.0f * amax;
+    if (!(b > 0.0f) || !(b < 3.0e38f)) return 1.0f;
+    int e;
+    frexpf(b, &e);  // 2^(e-1) <= b < 2^e
+    e = 15 - e;
+    e = e > 100 ? 100 : (e < -100 ? -100 : e);
+    return ldexpf(1.0f, e);
+}
+
+// V scales of the staged boards b0 .. b0+SB-1 (boards past the end: 1). x_amax holds one
+// max per board (per_board) or one bound for every board.
+__device__ __forceinline__ SetScale set_scale(const uint32_t *__restrict__ x_amax, int per_board, int b0, int n_boards) {
+    SetScale sc;
+#pragma unroll
+    for (int k = 0; k < SB; ++k) {
+        const int b = b0 + k;
+        const uint32_t bits = per_board ? (b < n_boards ? x_amax[b] : 0u) : x_amax[0];
+        sc.s[k] = pow2_scale(__builtin_bit_cast(float, bits));
+    }
+    return sc;
+}
+
+// MODE+4 phase stamps (core clocks, s_memtime) of workgroups 0..63, waves 0 and 4, first 8
+// chunks: per chunk [after load_x issue, after transform, after barrier+store_x, after GEMMs,
+// after epilogue, after closing barrier] relative to the chunk's start.
+#ifdef UTTT_DIAG_BUILD
+__device__ unsigned int g_stamp[64][2][8][6];
+#define UTTT_WINO3H_STAMP(b, w, g, k, v) (g_stamp[b][w][g][k] = (v))
+#else
+#define UTTT_WINO3H_STAMP(b, w, g, k, v) ((void)0)
+#endif
+
+// MODE (timing ablations only; 0 in the product): 1 skip the transform, 2 skip the
+// point GEMMs, 64 skip the fold, 512 plain (L2-allocating) input loads, 65536 nontemporal
+// residual loads, 131072 nontemporal output stores.
+// The product streams the conv input with nontemporal loads: 8 lanes read one whole 128-B
+// line, each line once per launch, and L2-allocating them would evict U (1.6 MB, re-read
+// per set) from the XCD's L2 (-4..6% at bench batch sizes). The epilogue's residual loads
+// and output stores are plain: one wave covers 64 B (16 channels) of a position's 512-B
+// row, so the two waves that share a 128-B line meet in L2 instead of each moving the line
+// to or from HBM (residual conv 106.7 -> 91.0 us at 1,344 boards, round 2,
+// tools/diag/wino3h_modes.py).
+template <bool RES, int MODE = 0, int PF = 3>
+__global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x, const uint16_t *__restrict__ u,
+                                                    float u_scale, const float *__restrict__ bias,
+                                                    const float *__restrict__ res, float *__restrict__ y,
+                                                    const uint32_t *__restrict__ x_amax, int x_amax_per_board,
+                                                    uint32_t *__restrict__ y_amax, uint32_t *__restrict__ amax_clear,
+                                                    int clear_count, int n_boards) {
+    // sX [padded position][channel] (border = 0) then sV
+    __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
+    float *const sX = reinterpret_cast<float *>(smem);
+    char *const sV = smem + XP * KC * 4;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // zero the per-board max row a later conv of this forward accumulates into
+    for (int i = (int)blockIdx.x * NT + tid; i < clear_count; i += (int)gridDim.x * NT) amax_clear[i] = 0u;
+    const int nsets = n_sets(n_boards);
+    if ((int)blockIdx.x >= nsets) return;
+    const int my_sets = (nsets - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = my_sets * NCH;
+    auto set_of = [&](int g) { return (int)blockIdx.x + (g / NCH) * (int)gridDim.x; };
+    auto set_b0 = [&](int g) { const int st = set_of(g); return GB * (st >> 1) + 3 * (st & 1); };  // first staged board
+    const int co4 = wv * 16 + 4 * (lane >> 4);  // the 4 output channels of this lane's MFMA results
+    const floatx4 bb4 = *reinterpret_cast<const floatx4 *>(bias + co4);
+
+    Acc S[15];
+#pragma unroll
+    for (int i = 0; i < 15; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+    const floatx2 k2 = {2.0f, 2.0f}, k4 = {4.0f, 4.0f};
+    float4 xr[XPT];
+    // MODE 256 (diagnostic): u holds 8 replicas, workgroup b reads replica b % 8
+    // MODE 8192 (diagnostic): replica (b / 8) % 8, i.e. the workgroups of one XCD spread over 8 copies
+    const uint16_t *ub = (MODE & 256)    ? u + (size_t)(blockIdx.x % 8) * (NP * C * C * 2)
+                         : (MODE & 8192) ? u + (size_t)((blockIdx.x >> 3) & 7) * (NP * C * C * 2)
+                                         : u;
+    const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(ub), 0, NP * C * C * 4, 0x00020000);
+    const int kq = lane >> 4;
+    const int voff = wv * 1024 + lane * 16;  // U fragment of lane (co, kq): lane-linear (uttt_nn_wino3h_weights)
+    // Every workgroup takes the chunks in the same order: the f32 accumulation order of a
+    // board's results must not depend on which workgroup (= where in the batch) it lands.
+    const int c_rot = 0;
+    auto chunk_of = [&](int g) { return (g % NCH + c_rot) % NCH; };
+    // 16-byte slot m ^ 2kq: conflict-free for both the transform's ds_write_b32 (32-lane groups,
+    // 32 banks) and the point loop's ds_read_b128 (lane groups {0-3,12-15,20-27}, ... of
+    // MI355X_MICROARCH.md §LDS); m ^ 4kq made the reads 2-way
+    const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (2 * kq)) * 16);
+
+    // zero the pads of sX (never written after this; the staged cells are rewritten every chunk):
+    // the 5 shared zero rows (10 positions each), the zero column of the 36 board rows, the last position
+    for (int i = fresh(tid); i < NPAD * (KC / 4); i += NT) {
+        const int j = i / (KC / 4), q = i % (KC / 4);
+        const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
+                      : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
+        reinterpret_cast<float4 *>(sX + pos * KC)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    __syncthreads();
+    BFrag bq[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, c_rot, voff);
+    load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
+    SetScale sc = set_scale(x_amax, x_amax_per_board, set_b0(0), n_boards);  // V scales of the current set
+    store_x(sX, xr, sc, tid);
+    __syncthreads();
+    const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
+    auto mark = [&](int g, int k, unsigned long long t0) {
+        if (stamp && g < 8) UTTT_WINO3H_STAMP(blockIdx.x, tid >> 8, g, k, (unsigned int)(__builtin_amdgcn_s_memtime() - t0));
+    };
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+        const int c = g % NCH, ch = chunk_of(g);
+        const unsigned long long t0 = (MODE & 4) ? __builtin_amdgcn_s_memtime() : 0ull;
+        // the next chunk's inputs load during this chunk's transform (registers are
+        // free then; the point loop needs nearly all of them)
+        if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+        // the next chunk's V scales: this set's, or the next set's after its last chunk
+        SetScale sc_next = sc;
+        if (c == NCH - 1 && g + 1 < G) sc_next = set_scale(x_amax, x_amax_per_board, set_b0(g + 1), n_boards);
+        mark(g, 0, t0);
+        if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid), set_of(g) & 1);
+        mark(g, 1, t0);
+        lds_barrier();
+        if (g + 1 < G) store_x(sX, xr, sc_next, fresh(tid));
+        mark(g, 2, t0);
+        if constexpr ((MODE & 3) != 2) {
+            AFrag a0;
+            if constexpr (!(MODE & kNoALookahead)) a0 = load_a(sv_lane, 0);
+            floatx2 mprev[4];
+            xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff);
+        }
+        mark(g, 3, t0);
+        if (c == NCH - 1) {
+            // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
+            // of tile slot 16rt + (lane & 15)
+            const int st = set_of(g), grp = st >> 1, h = st & 1;
+            const int el = fresh(lane);
+            // Straight from registers: the MFMA output puts 4 consecutive channels of one tile
+            // in a lane (U is the A operand), so every output position is one 16-byte store
+            // (+ one 16-byte residual load, issued before Y is formed); no LDS round trip and
+            // no barrier.
+            size_t off[2];
+            bool live[2];
+            int board_of[2];
+            float inv[2];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const int gt = 32 * h + 16 * rt + (el & 15), gb = gt / 9, tt = gt - 9 * gb;
+                const int board = GB * grp + gb;
+                live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
+                // this lane's 4 output channels, recomputed here rather than kept live (spilled) over the loop
+                const int co4e = (fresh(tid) >> 6) * 16 + 4 * (el >> 4);
+                off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4e;
+                board_of[rt] = board;
+                // this tile's board's V scale times su: both powers of two, so 1/x is exact
+                inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
+            }
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                float vmax = 0.0f;
+                // tile block rt: residual loads first (in flight while Y is formed)
+                floatx4 rv[9];
+                if constexpr (RES) {
+#pragma unroll
+                    for (int ab = 0; ab < 9; ++ab) {
+                        rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+                        if (live[rt]) {
+                            const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+                            rv[ab] = (MODE & 65536) ? __builtin_nontemporal_load(src) : *src;
+                        }
+                    }
+                }
+                floatx4 Y[9];
+#pragma unroll
+                for (int ab = 0; ab < 9; ++ab) {
+                    const int a = ab / 3, b = ab % 3;
+                    floatx4 acc = {};
+#pragma unroll
+                    for (int v = 0; v < 5; ++v) {
+                        if (at(b, v) == 0) continue;
+                        const Acc &q = S[a * 5 + v];
+                        const floatx4 s4 = {q.p[2 * rt].x, q.p[2 * rt].y, q.p[2 * rt + 1].x, q.p[2 * rt + 1].y};
+                        acc = at(b, v) == 1 ? acc + s4
+                            : at(b, v) == -1 ? acc - s4
+                                             : __builtin_elementwise_fma(floatx4((float)at(b, v)), s4, acc);
+                    }
+                    Y[ab] = acc;
+                }
+#pragma unroll
+                for (int i = 0; i < 15; ++i) {
+                    S[i].p[2 * rt] = floatx2{0.0f, 0.0f};
+                    S[i].p[2 * rt + 1] = floatx2{0.0f, 0.0f};
+                }
+#pragma unroll
+                for (int ab = 0; ab < 9 && live[rt]; ++ab) {
+                    floatx4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv[rt], bb4[r]);
+                    if constexpr (RES) v += rv[ab];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.0f);
+                    floatx4 *dst = reinterpret_cast<floatx4 *>(y + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+                    if constexpr (MODE & 8) {  // diagnostic: no output stores (kept live)
+                        asm volatile("" ::"v"(v));
+                    } else if constexpr (MODE & 131072) {
+                        __builtin_nontemporal_store(v, dst);
+                    } else {
+                        *dst = v;
+                    }
+                    vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+                }
+                if (y_amax) {
+                    // the 4 lanes of a tile (lane bits 4-5: channel quads) -> one max per tile,
+                    // then one atomic per (tile, wave) into its board's slot
+                    vmax = fmaxf(vmax, __shfl_xor(vmax, 16));
+                    vmax = fmaxf(vmax, __shfl_xor(vmax, 32));
+                    if (el < 16 && live[rt])  // v >= 0: u32 bit order = value order
+                        atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
+                }
+            }
+        }
+        sc = sc_next;
+        mark(g, 4, t0);
+        lds_barrier();
+        mark(g, 5, t0);
+    }
+}
+
+// |x| maximum into *amax (u32 float bits; the caller zeroes it first)
+__global__ __launch_bounds__(256) void k_amax(const float *__restrict__ x, int64_t count, uint32_t *__restrict__ amax) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
+        m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(uint32_t, m));
+}
+
+static int grid_size(int n_boards) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+    }
+    const int nsets = n_sets(n_boards);
+    return nsets < cus ? nsets : cus;
+}
+
+}  // namespace wino3h
+}  // namespace uttt

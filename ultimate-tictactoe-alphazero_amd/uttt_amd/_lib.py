@@ -119,6 +119,22 @@ def load():
     return _lib
 
 
+_diag = None
+
+
+def load_diag():
+    """The diagnostics library (libuttt_diag.so, `make -C <pkg> diag`): conv timing ablations and phase
+    stamps for tools/diag. Never loaded by the product path or the tests."""
+    global _diag
+    if _diag is None:
+        load()
+        path = os.path.join(os.path.dirname(LIB_PATH), "libuttt_diag.so")
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not built: run `make -C {PKG_ROOT} diag`")
+        _diag = ctypes.CDLL(path)
+    return _diag
+
+
 def check(rc):
     if rc != UTTT_OK:
         msg = load().uttt_last_error().decode(errors="replace")
