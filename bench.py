@@ -554,7 +554,7 @@ def main():
                                                 "levels (node header -> child stats -> next node); us_per_level is "
                                                 "the launch time divided by that chain"}),
             "roofline_backup": hbm_roofline("k_apply (expand + backup, one wave per pending leaf)", st["apply"],
-                                            r["trees_per_launch"]),
+                                            r["trees_per_launch"], "pmc_apply.json"),
             "nn": {"rows_evaluated": r["rows"], "ms": round(r["nn_ms"], 2),
                    "share_of_step": round(r["nn_ms"] / 1e3 / r["elapsed"], 4),
                    "lane_sum_ms": round(r["nn_lane_sum_ms"], 2),

@@ -25,7 +25,9 @@ sys.path[:0] = [REPO, PKG]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workdir", default=os.path.join(REPO, "gpurun_out", "cycle_wd"))
+    import tempfile
+    ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "uttt_cycle_wd"),
+                    help="scratch working directory (./model, ./data); outside gpurun_out (64 MiB cap)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--games", type=int, default=None, help="SP_GAME_COUNT override (default: the reference's 500)")
     ap.add_argument("--epochs", type=int, default=None, help="RN_EPOCHS override (default: the reference's 100)")
@@ -56,7 +58,8 @@ def main():
                       "MCTS_BATCH_SIZE": self_play_cpp.MCTS_BATCH_SIZE, "RN_EPOCHS": train_network.RN_EPOCHS,
                       "BATCH_SIZE": train_network.BATCH_SIZE, "EN_GAME_COUNT": evaluate_network.EN_GAME_COUNT,
                       "EP_GAME_COUNT": evaluate_best_player.EP_GAME_COUNT},
-           "n_gpus": 1, "device": torch.cuda.get_device_name(0), "phases": {}}
+           "n_gpus": 1, "device": torch.cuda.get_device_name(0), "phases": {},
+           "train_precision": os.environ.get("UTTT_TRAIN_PRECISION", "fp32")}
     out["import_s"] = round(time.perf_counter() - t_import, 3)
     torch.manual_seed(0)
     np.random.seed(0)

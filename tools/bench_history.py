@@ -21,7 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--games", type=int, default=32768)
     ap.add_argument("--plies", type=int, default=58)
-    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "bench_history.history"))
+    import tempfile
+    ap.add_argument("--out", default=os.path.join(tempfile.gettempdir(), "bench_history.history"))
     ap.add_argument("--keep", action="store_true")
     args = ap.parse_args()
     import numpy as np

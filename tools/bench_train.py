@@ -32,8 +32,9 @@ def main():
     ap.add_argument("--samples", type=int, default=29000)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--cpu-steps", type=int, default=20)
-    ap.add_argument("--variants", default="eager,graph,graph_cl")
-    ap.add_argument("--benchmark", type=int, default=1, help="torch.backends.cudnn.benchmark (MIOpen find)")
+    ap.add_argument("--variants", default="eager,graph,graph_f16,graph_f16_cl")
+    ap.add_argument("--benchmark", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen find) for the "
+                                                                "eager variants; the graph step always captures immediate mode")
     args = ap.parse_args()
     import torch
     from uttt_amd import train
@@ -43,11 +44,13 @@ def main():
     dev = torch.device("cuda", 0)
     steps = args.epochs * -(-args.samples // train.BATCH_SIZE)
     out = {"metric": "train_network samples/s (DualNetwork 128f x16 fp32, batch 128, Adam)", "unit": "samples/s",
-           "n_gpus": 1, "epochs": args.epochs, "steps": steps, "dtype": "f32",
+           "n_gpus": 1, "epochs": args.epochs, "steps": steps,
+           "dtype": "f32; *_f16 variants: convolutions and linear layers on f16 operands with f32 accumulation (TF32-class mantissa), BatchNorm, softmax and loss in f32",
            "data": f"synthetic history of {args.samples} plies", "variants": {}}
     for var in args.variants.split(","):
         kw = {"eager": dict(graph=False), "graph": dict(graph=True), "graph_cl": dict(graph=True, channels_last=True),
-              "eager_cl": dict(graph=False)}[var]
+              "graph_f16": dict(graph=True, precision="f16"),
+              "graph_f16_cl": dict(graph=True, precision="f16", channels_last=True)}[var]
         model = random_network(0)
         train.train_network(model, h[:1024], epochs=1, device=dev, log=None, **kw)  # warm-up (MIOpen tuning)
         model = random_network(0)

@@ -33,7 +33,7 @@ def main():
     _lib.load()
     dlib = _lib.load_diag()
     f = dlib.uttt_diag_wino3h_variant
-    f.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 5 + [ctypes.c_int32] * 2 + \
+    f.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 4 + [ctypes.c_int32] * 2 + \
         [ctypes.c_void_p]
     f.restype = ctypes.c_int
     net = random_network(0)
@@ -41,7 +41,7 @@ def main():
     uh, su = wino3h_weights(w)
     uh, b = uh.cuda(), b.cuda()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    variants = [int(v) for v in os.environ.get("VARIANTS", "1,6").split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", "1,6").split(",") if v]
     rounds = int(os.environ.get("ROUNDS", "3"))
     for n in [int(a) for a in (sys.argv[1:] or ["1344", "2688", "16384"])]:
         g = torch.Generator(device="cuda").manual_seed(n)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""k_select HBM traffic per launch from tools/pmc_select.sh output -> profiles/<round>/pmc_select.json.
+"""k_select (or k_apply) HBM traffic per launch from tools/pmc_select.sh output -> profiles/<round>/pmc_select.json.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3); steady state = the
 last third of the k_select dispatches of each pass. Raw values: on gfx950
@@ -7,7 +7,7 @@ FETCH_SIZE counts 64 B per 128-B read request (MI355X_MICROARCH.md, HBM), i.e.
 it can under-report wide coalesced reads by 2x; k_select's reads are 4 B/lane
 and uncalibrated, so both the raw and the doubled read figure are kept.
 
-usage: pmc_summary.py PMC_DIR BENCH_LOG OUT.json
+usage: pmc_summary.py PMC_DIR BENCH_LOG OUT.json [KERNEL]   (k_select default, or k_apply)
 """
 import csv
 import json
@@ -21,20 +21,21 @@ def per_launch(path, counter, kernel="k_select"):
     return sum(v) / len(v), len(v)
 
 
-def main(d, bench_log, out):
-    fetch, nf = per_launch(f"{d}/p1/t_counter_collection.csv", "FETCH_SIZE")
-    write, nw = per_launch(f"{d}/p2/t_counter_collection.csv", "WRITE_SIZE")
-    rdreq, _ = per_launch(f"{d}/p3/t_counter_collection.csv", "TCC_EA0_RDREQ_sum")
+def main(d, bench_log, out, kernel="k_select"):
+    fetch, nf = per_launch(f"{d}/p1/t_counter_collection.csv", "FETCH_SIZE", kernel)
+    write, nw = per_launch(f"{d}/p2/t_counter_collection.csv", "WRITE_SIZE", kernel)
+    rdreq, _ = per_launch(f"{d}/p3/t_counter_collection.csv", "TCC_EA0_RDREQ_sum", kernel)
     bench = json.loads([ln for ln in open(bench_log).read().splitlines() if ln.startswith("{")][-1])
+    roof = bench["roofline"] if kernel == "k_select" else bench["roofline_backup"]
     res = {
-        "kernel": "k_select",
+        "kernel": kernel,
         "launches_averaged": [nf, nw],
         "trees_per_launch": bench["config"]["games_per_gpu"] // bench["config"].get("lanes_per_gpu", 1),
         "fetch_bytes": fetch * 1024, "write_bytes": write * 1024,
         "tcc_ea0_rdreq_x64_bytes": rdreq * 64,
         "traffic_bytes_raw": (fetch + write) * 1024,
         "traffic_bytes_reads_doubled": (2 * fetch + write) * 1024,
-        "algo_bytes_per_launch_bench": bench["roofline"]["algo_bytes_per_launch"],
+        "algo_bytes_per_launch_bench": roof["algo_bytes_per_launch"],
         "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE, then WRITE_SIZE, then TCC_EA0_RDREQ_sum, "
                   "separate passes of `bench.py --steps 6 --warmup 2 --age 40`; KiB -> bytes",
     }
@@ -44,4 +45,4 @@ def main(d, bench_log, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

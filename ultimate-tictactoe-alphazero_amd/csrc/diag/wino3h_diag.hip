@@ -8,6 +8,7 @@
 
 #include "uttt_nn.h"
 #include "wino3h_impl.h"
+#include "wino3p_impl.h"
 
 using namespace uttt;
 
@@ -22,6 +23,9 @@ static void ablation_res(const float *x, const uint16_t *u, float u_scale, const
 }
 
 extern "C" {
+
+int uttt_diag_wino3h_scalar(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *res,
+                            float *y, const uint32_t *x_amax, int32_t n_boards, void *stream);
 
 // Diagnostic: the residual tensor of the ablation's residual form (null: x itself)
 void uttt_diag_wino3h_set_residual(const float *res) { g_diag_res = res; }
@@ -94,6 +98,15 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
             hipLaunchKernelGGL((k_wino3h_conv<false, M, P>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y,   \
                                x_amax, 1, nullptr, nullptr, 0, n_boards);                                            \
     } while (0)
+#define UTTT_P(PF_, ALA_)                                                                                              \
+    do {                                                                                                              \
+        if (res)                                                                                                      \
+            hipLaunchKernelGGL((k_wino3p_conv<true, PF_, ALA_>), grid, dim3(NT), 0, st, x, u, u_scale, bias, res, y,   \
+                               x_amax, 1, nullptr, nullptr, 0, n_boards);                                            \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_wino3p_conv<false, PF_, ALA_>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, \
+                               y, x_amax, 1, nullptr, nullptr, 0, n_boards);                                         \
+    } while (0)
     switch (variant) {
         case 1: UTTT_V(kBufferX, 3); break;
         case 2: UTTT_V(kNoALookahead, 4); break;
@@ -101,9 +114,16 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
         case 4: UTTT_V(kBufferX | kNoALookahead, 4); break;
         case 5: UTTT_V(kBufferX | kNoALookahead, 5); break;
         case 6: UTTT_V(kNoALookahead, 3); break;
+        case 20: UTTT_V(kFoldBuiltin, 3); break;
+        case 22: return uttt_diag_wino3h_scalar(x, u, u_scale, bias, res, y, x_amax, n_boards, stream);
+        case 10: UTTT_P(3, true); break;
+        case 11: UTTT_P(3, false); break;
+        case 12: UTTT_P(2, true); break;
+        case 13: UTTT_P(4, false); break;
         default: UTTT_V(0, 3);
     }
 #undef UTTT_V
+#undef UTTT_P
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }
 

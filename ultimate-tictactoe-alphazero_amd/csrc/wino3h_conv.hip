@@ -52,6 +52,21 @@ namespace uttt {
 void set_error(const char *fmt, ...);
 }
 
+namespace uttt {
+namespace wino3h {
+// |x| maximum into *amax (u32 float bits; the caller zeroes it first)
+__global__ __launch_bounds__(256) void k_amax(const float *__restrict__ x, int64_t count, uint32_t *__restrict__ amax) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
+        m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(uint32_t, m));
+}
+
+}  // namespace wino3h
+}  // namespace uttt
+
 using namespace uttt;
 
 extern "C" {

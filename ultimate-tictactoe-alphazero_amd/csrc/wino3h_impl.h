@@ -52,6 +52,12 @@ __host__ __device__ constexpr int at(int a, int u) {
     return m[a][u];
 }
 
+// Variant bits (diagnostic builds; the product is MODE 0)
+constexpr int kNoALookahead = 1 << 21;  // V fragments read at their own point (frees 16 VGPRs for U prefetch)
+constexpr int kBufferX = 1 << 22;       // input loads as buffer loads, zero beyond the batch: no branches
+constexpr int kFoldBuiltin = 1 << 23;   // fold as compiler-visible ops (hazards padded by the compiler)
+constexpr int kFoldScalar = 1 << 24;    // ... as scalar v_add_f32 / v_fma_f32 pairs (TU built with -fno-slp-vectorize)
+
 struct Acc {
     floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
 };
@@ -82,7 +88,23 @@ __device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], flo
         // MFMA, between producer and reader, and the output bits equal those of a compiler-visible
         // fold (builtin packed ops, hazard-padded; 7% slower from spills) on the same inputs
         // (round 2, tools/diag/wino3h_modes.py).
-        if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
+        if constexpr (MODE & kFoldScalar) {
+            floatx2 &t = S[a * 5 + v].p[j];
+            if constexpr (K == 1) {
+                t.x = t.x + m[j].x;
+                t.y = t.y + m[j].y;
+            } else if constexpr (K == -1) {
+                t.x = t.x - m[j].x;
+                t.y = t.y - m[j].y;
+            } else {
+                t.x = __builtin_fmaf(m[j].x, (float)K, t.x);
+                t.y = __builtin_fmaf(m[j].y, (float)K, t.y);
+            }
+        } else if constexpr (MODE & kFoldBuiltin) {
+            if constexpr (K == 1) S[a * 5 + v].p[j] = S[a * 5 + v].p[j] + m[j];
+            else if constexpr (K == -1) S[a * 5 + v].p[j] = S[a * 5 + v].p[j] - m[j];
+            else S[a * 5 + v].p[j] = __builtin_elementwise_fma(m[j], K == 2 ? k2 : k4, S[a * 5 + v].p[j]);
+        } else if constexpr (K == 1) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
         else if constexpr (K == -1)
             asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]));
         else if constexpr (K == 2) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(S[a * 5 + v].p[j]) : "v"(m[j]), "v"(k2));
@@ -143,10 +165,6 @@ __device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
     a.l1 = *reinterpret_cast<const halfx8 *>(p + 3 * VPLANE);
     return a;
 }
-
-// Variant bits (diagnostic builds; the product is MODE 0)
-constexpr int kNoALookahead = 1 << 21;  // V fragments read at their own point (frees 16 VGPRs for U prefetch)
-constexpr int kBufferX = 1 << 22;       // input loads as buffer loads, zero beyond the batch: no branches
 
 // Point loop, software-pipelined: B PF points ahead (L2), A one point ahead (LDS).
 // The fold of point XI-1 is issued among point XI's MFMAs.
@@ -403,6 +421,101 @@ __device__ __forceinline__ SetScale set_scale(const uint32_t *__restrict__ x_ama
     return sc;
 }
 
+// After a set's last chunk: Y[a][b] = sum_v S[a][v] A^T[b][v], scale, bias, residual, ReLU, one 16-byte
+// store per output position straight from registers, per-board output max; S is zeroed for the next set.
+template <bool RES, int MODE>
+__device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScale &sc, float u_scale, floatx4 bb4,
+                                             const float *__restrict__ res, float *__restrict__ y,
+                                             uint32_t *__restrict__ y_amax, int n_boards, int tid, int lane) {
+    // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
+    // of tile slot 16rt + (lane & 15)
+    const int grp = st >> 1, h = st & 1;
+    const int el = fresh(lane);
+    // Straight from registers: the MFMA output puts 4 consecutive channels of one tile
+    // in a lane (U is the A operand), so every output position is one 16-byte store
+    // (+ one 16-byte residual load, issued before Y is formed); no LDS round trip and
+    // no barrier.
+    size_t off[2];
+    bool live[2];
+    int board_of[2];
+    float inv[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int gt = 32 * h + 16 * rt + (el & 15), gb = gt / 9, tt = gt - 9 * gb;
+        const int board = GB * grp + gb;
+        live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
+        // this lane's 4 output channels, recomputed here rather than kept live (spilled) over the loop
+        const int co4e = (fresh(tid) >> 6) * 16 + 4 * (el >> 4);
+        off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4e;
+        board_of[rt] = board;
+        // this tile's board's V scale times su: both powers of two, so 1/x is exact
+        inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        float vmax = 0.0f;
+        // tile block rt: residual loads first (in flight while Y is formed)
+        floatx4 rv[9];
+        if constexpr (RES) {
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab) {
+                rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+                if (live[rt]) {
+                    const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+                    rv[ab] = (MODE & 65536) ? __builtin_nontemporal_load(src) : *src;
+                }
+            }
+        }
+        floatx4 Y[9];
+#pragma unroll
+        for (int ab = 0; ab < 9; ++ab) {
+            const int a = ab / 3, b = ab % 3;
+            floatx4 acc = {};
+#pragma unroll
+            for (int v = 0; v < 5; ++v) {
+                if (at(b, v) == 0) continue;
+                const Acc &q = S[a * 5 + v];
+                const floatx4 s4 = {q.p[2 * rt].x, q.p[2 * rt].y, q.p[2 * rt + 1].x, q.p[2 * rt + 1].y};
+                acc = at(b, v) == 1 ? acc + s4
+                    : at(b, v) == -1 ? acc - s4
+                                     : __builtin_elementwise_fma(floatx4((float)at(b, v)), s4, acc);
+            }
+            Y[ab] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < 15; ++i) {
+            S[i].p[2 * rt] = floatx2{0.0f, 0.0f};
+            S[i].p[2 * rt + 1] = floatx2{0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int ab = 0; ab < 9 && live[rt]; ++ab) {
+            floatx4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv[rt], bb4[r]);
+            if constexpr (RES) v += rv[ab];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.0f);
+            floatx4 *dst = reinterpret_cast<floatx4 *>(y + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+            if constexpr (MODE & 8) {  // diagnostic: no output stores (kept live)
+                asm volatile("" ::"v"(v));
+            } else if constexpr (MODE & 131072) {
+                __builtin_nontemporal_store(v, dst);
+            } else {
+                *dst = v;
+            }
+            vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+        }
+        if (y_amax) {
+            // the 4 lanes of a tile (lane bits 4-5: channel quads) -> one max per tile,
+            // then one atomic per (tile, wave) into its board's slot
+            vmax = fmaxf(vmax, __shfl_xor(vmax, 16));
+            vmax = fmaxf(vmax, __shfl_xor(vmax, 32));
+            if (el < 16 && live[rt])  // v >= 0: u32 bit order = value order
+                atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
+        }
+    }
+}
+
 // MODE+4 phase stamps (core clocks, s_memtime) of workgroups 0..63, waves 0 and 4, first 8
 // chunks: per chunk [after load_x issue, after transform, after barrier+store_x, after GEMMs,
 // after epilogue, after closing barrier] relative to the chunk's start.
@@ -513,110 +626,12 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff);
         }
         mark(g, 3, t0);
-        if (c == NCH - 1) {
-            // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
-            // of tile slot 16rt + (lane & 15)
-            const int st = set_of(g), grp = st >> 1, h = st & 1;
-            const int el = fresh(lane);
-            // Straight from registers: the MFMA output puts 4 consecutive channels of one tile
-            // in a lane (U is the A operand), so every output position is one 16-byte store
-            // (+ one 16-byte residual load, issued before Y is formed); no LDS round trip and
-            // no barrier.
-            size_t off[2];
-            bool live[2];
-            int board_of[2];
-            float inv[2];
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) {
-                const int gt = 32 * h + 16 * rt + (el & 15), gb = gt / 9, tt = gt - 9 * gb;
-                const int board = GB * grp + gb;
-                live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
-                // this lane's 4 output channels, recomputed here rather than kept live (spilled) over the loop
-                const int co4e = (fresh(tid) >> 6) * 16 + 4 * (el >> 4);
-                off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4e;
-                board_of[rt] = board;
-                // this tile's board's V scale times su: both powers of two, so 1/x is exact
-                inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
-            }
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) {
-                float vmax = 0.0f;
-                // tile block rt: residual loads first (in flight while Y is formed)
-                floatx4 rv[9];
-                if constexpr (RES) {
-#pragma unroll
-                    for (int ab = 0; ab < 9; ++ab) {
-                        rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-                        if (live[rt]) {
-                            const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
-                            rv[ab] = (MODE & 65536) ? __builtin_nontemporal_load(src) : *src;
-                        }
-                    }
-                }
-                floatx4 Y[9];
-#pragma unroll
-                for (int ab = 0; ab < 9; ++ab) {
-                    const int a = ab / 3, b = ab % 3;
-                    floatx4 acc = {};
-#pragma unroll
-                    for (int v = 0; v < 5; ++v) {
-                        if (at(b, v) == 0) continue;
-                        const Acc &q = S[a * 5 + v];
-                        const floatx4 s4 = {q.p[2 * rt].x, q.p[2 * rt].y, q.p[2 * rt + 1].x, q.p[2 * rt + 1].y};
-                        acc = at(b, v) == 1 ? acc + s4
-                            : at(b, v) == -1 ? acc - s4
-                                             : __builtin_elementwise_fma(floatx4((float)at(b, v)), s4, acc);
-                    }
-                    Y[ab] = acc;
-                }
-#pragma unroll
-                for (int i = 0; i < 15; ++i) {
-                    S[i].p[2 * rt] = floatx2{0.0f, 0.0f};
-                    S[i].p[2 * rt + 1] = floatx2{0.0f, 0.0f};
-                }
-#pragma unroll
-                for (int ab = 0; ab < 9 && live[rt]; ++ab) {
-                    floatx4 v;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv[rt], bb4[r]);
-                    if constexpr (RES) v += rv[ab];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.0f);
-                    floatx4 *dst = reinterpret_cast<floatx4 *>(y + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
-                    if constexpr (MODE & 8) {  // diagnostic: no output stores (kept live)
-                        asm volatile("" ::"v"(v));
-                    } else if constexpr (MODE & 131072) {
-                        __builtin_nontemporal_store(v, dst);
-                    } else {
-                        *dst = v;
-                    }
-                    vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
-                }
-                if (y_amax) {
-                    // the 4 lanes of a tile (lane bits 4-5: channel quads) -> one max per tile,
-                    // then one atomic per (tile, wave) into its board's slot
-                    vmax = fmaxf(vmax, __shfl_xor(vmax, 16));
-                    vmax = fmaxf(vmax, __shfl_xor(vmax, 32));
-                    if (el < 16 && live[rt])  // v >= 0: u32 bit order = value order
-                        atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
-                }
-            }
-        }
+        if (c == NCH - 1) set_epilogue<RES, MODE>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane);
         sc = sc_next;
         mark(g, 4, t0);
         lds_barrier();
         mark(g, 5, t0);
     }
-}
-
-// |x| maximum into *amax (u32 float bits; the caller zeroes it first)
-__global__ __launch_bounds__(256) void k_amax(const float *__restrict__ x, int64_t count, uint32_t *__restrict__ amax) {
-    float m = 0.0f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
-        m = fmaxf(m, fabsf(x[i]));
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(uint32_t, m));
 }
 
 static int grid_size(int n_boards) {

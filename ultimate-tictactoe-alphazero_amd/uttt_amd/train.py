@@ -101,24 +101,38 @@ class GraphedStep:
     caller's weights exactly as the eager loop does. The graph adds the step's loss to a device
     accumulator; batches of another size (an epoch's last) run the same body eagerly."""
 
-    def __init__(self, model, opt, x, p, v, batch_size, channels_last=False):
+    def __init__(self, model, opt, x, p, v, batch_size, channels_last=False, precision="fp32"):
         self.model, self.opt, self.x, self.p, self.v = model, opt, x, p, v
         self.channels_last = channels_last
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}")
+        self.precision = precision
         dev = x.device
         self.idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
         self.loss_sum = torch.zeros((), device=dev)
+        if precision == "f16":
+            # static loss scale; a step whose unscaled gradients hold an inf / nan is skipped on the
+            # device (fused Adam reads found_inf), so nothing in the step needs the host
+            self.scale = float(F16_LOSS_SCALE)
+            self.inv_scale = torch.full((), 1.0 / F16_LOSS_SCALE, device=dev)
+            self.found_inf = torch.zeros((), device=dev)
+            opt.found_inf = self.found_inf
         snap = {k: t.detach().clone() for k, t in model.state_dict().items()}
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(3):  # allocator, MIOpen kernel choice, optimiser state
-                opt.zero_grad(set_to_none=True)
+        # MIOpen's immediate mode (heuristic kernel choice), whatever torch.backends.cudnn.benchmark
+        # says (the reference's dual_network.py sets it at import): with find mode the captured step
+        # ran 7x slower and trained to a different loss (round 3, tools/bench_train.py)
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=False):
+            with torch.cuda.stream(side):
+                for _ in range(3):  # allocator, MIOpen kernel choice, optimiser state
+                    opt.zero_grad(set_to_none=True)
+                    self._body(self.idx)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            opt.zero_grad(set_to_none=True)
+            with torch.cuda.graph(self.graph):
                 self._body(self.idx)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
-            self._body(self.idx)
         # undo the warm-up: the same tensors (the graph's addresses), the caller's values
         with torch.no_grad():
             for k, t in model.state_dict().items():
@@ -133,10 +147,21 @@ class GraphedStep:
         xb = self.x.index_select(0, idx)
         if self.channels_last:
             xb = xb.contiguous(memory_format=torch.channels_last)
-        pred_p, pred_v = self.model(xb)
+        if self.precision == "f16":
+            with torch.autocast("cuda", dtype=torch.float16):
+                pred_p, pred_v = self.model(xb)
+            pred_p, pred_v = pred_p.float(), pred_v.float()
+        else:
+            pred_p, pred_v = self.model(xb)
         loss = policy_loss_fn(pred_p, self.p.index_select(0, idx)) + \
             nn.functional.mse_loss(pred_v, self.v.index_select(0, idx))
-        loss.backward()
+        if self.precision == "f16":
+            (loss * self.scale).backward()
+            self.found_inf.zero_()
+            grads = [q.grad for q in self.model.parameters() if q.grad is not None]
+            torch._amp_foreach_non_finite_check_and_unscale_(grads, self.found_inf, self.inv_scale)
+        else:
+            loss.backward()
         self.opt.step()
         self.loss_sum += loss.detach()
         return loss
@@ -147,7 +172,14 @@ class GraphedStep:
             self.graph.replay()
         else:
             self.opt.zero_grad(set_to_none=False)
-            self._body(idx)
+            with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=False):
+                self._body(idx)
+
+
+PRECISIONS = ("fp32", "f16")
+# "f16": convolutions and linear layers on f16 operands (10-bit mantissa, the reference's cuDNN TF32
+# default on its NVIDIA card has the same), f32 accumulation, BatchNorm / softmax / loss in f32
+F16_LOSS_SCALE = 2.0 ** 12
 
 
 def _use_graph(graph, device, world):
@@ -158,7 +190,7 @@ def _use_graph(graph, device, world):
 
 
 def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, device=None, seed=0, lr=0.001,
-                  log=print, sync_bn=None, graph=None, channels_last=False):
+                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None):
     """Train `model` (a DualNetwork) on `history` in place; returns the per-epoch mean losses.
     In a torch.distributed job every rank calls this with the same history and seed.
     graph (default on for one GPU; UTTT_TRAIN_GRAPH=0 disables): replay the step as a HIP graph
@@ -167,8 +199,13 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
     device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
                         else torch.device("cpu"))
     x, p, v = (torch.from_numpy(a).to(device) for a in history_arrays(history))  # resident in HBM
+    if precision is None:
+        import os
+        precision = os.environ.get("UTTT_TRAIN_PRECISION", "fp32")
     if _use_graph(graph, device, world):
-        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last)
+        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision)
+    if precision != "fp32":
+        raise ValueError("precision other than fp32 needs the graph step (one GPU)")
     net = prepare(model, device, sync_bn)
     opt = torch.optim.Adam(net.parameters(), lr=lr)
     sched = torch.optim.lr_scheduler.LambdaLR(opt, lr_lambda=lr_lambda)
@@ -192,14 +229,17 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
     return losses
 
 
-def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last):
+def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision="fp32"):
     net = model.to(device)
     if channels_last:
         net = net.to(memory_format=torch.channels_last)
     net.train()
     lr_t = torch.tensor(lr, dtype=torch.float32, device=device)
-    opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, foreach=True)
-    step = GraphedStep(net, opt, x, p, v, batch_size, channels_last)
+    if precision == "f16":  # the fused kernel takes found_inf (skips the step on the device)
+        opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, fused=True)
+    else:
+        opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, foreach=True)
+    step = GraphedStep(net, opt, x, p, v, batch_size, channels_last, precision)
     losses = []
     for epoch in range(epochs):
         lr_t.fill_(lr * lr_lambda(epoch))
@@ -218,5 +258,5 @@ def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, ch
     return losses
 
 
-__all__ = ["BATCH_SIZE", "GraphedStep", "RN_EPOCHS", "batches", "history_arrays", "local_slice", "lr_lambda",
+__all__ = ["BATCH_SIZE", "F16_LOSS_SCALE", "GraphedStep", "PRECISIONS", "RN_EPOCHS", "batches", "history_arrays", "local_slice", "lr_lambda",
            "policy_loss_fn", "prepare", "train_network", "train_step"]
