@@ -468,6 +468,10 @@ def main():
                         ("c3_4096x400", dict(sims=400, age=30, warmup=2, steps=4)),
                         # BASELINE configs[1]: 1,024 games x 50 sims, MCTS_BATCH_SIZE 1024 (one flush per move)
                         ("c2_1024x50_b1024", dict(games=1024, batch=1024, age=100)),
+                        # the same without the evaluation cache: with B >= S every tree flushes one leaf
+                        # per move, and the one-hot scores make every game play the same line, so the cache
+                        # answers every leaf above; off, each move is one network call on 1,024 boards
+                        ("c2_1024x50_b1024_cache_off", dict(games=1024, batch=1024, age=100, cache_log2=0)),
                         # SURVEY §8(d) kernel microbench: the search kernels alone (hash evaluator, no network)
                         ("tree_only_4096x50", dict(evaluator="hash", age=100)),
                         ("tree_only_4096x400", dict(evaluator="hash", sims=400, age=30, warmup=2, steps=4))):

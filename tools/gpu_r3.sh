@@ -24,6 +24,10 @@ for s in $STEPS; do
     hist)  timeout -k 10 300 python -u tools/bench_history.py > $OUT/history.log 2>&1 ;;
     pmcsel) timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 ;;
     pmcsq) timeout -k 10 600 bash tools/pmc_sq.sh > $OUT/pmc_sq.log 2>&1 ;;
+    tprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tprof -o train \
+               -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \
+               > $OUT/tprof.log 2>&1 ;;
+    tcomp) timeout -k 10 600 python -u tools/diag/train_compare.py > $OUT/train_compare.log 2>&1 ;;
     tcheck) timeout -k 10 300 python -u tools/diag/train_graph_check.py > $OUT/train_check.log 2>&1 ;;
     vars)  timeout -k 10 300 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
     bench) timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 ;;

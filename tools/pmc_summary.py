@@ -26,7 +26,7 @@ def main(d, bench_log, out, kernel="k_select"):
     write, nw = per_launch(f"{d}/p2/t_counter_collection.csv", "WRITE_SIZE", kernel)
     rdreq, _ = per_launch(f"{d}/p3/t_counter_collection.csv", "TCC_EA0_RDREQ_sum", kernel)
     bench = json.loads([ln for ln in open(bench_log).read().splitlines() if ln.startswith("{")][-1])
-    roof = bench["roofline"] if kernel == "k_select" else bench["roofline_backup"]
+    roof = bench["roofline_select"] if kernel == "k_select" else bench["roofline_backup"]
     res = {
         "kernel": kernel,
         "launches_averaged": [nf, nw],

@@ -9,6 +9,7 @@
 #include "uttt_nn.h"
 #include "wino3h_impl.h"
 #include "wino3p_impl.h"
+#include "wino3q_impl.h"
 
 using namespace uttt;
 
@@ -98,6 +99,15 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
             hipLaunchKernelGGL((k_wino3h_conv<false, M, P>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y,   \
                                x_amax, 1, nullptr, nullptr, 0, n_boards);                                            \
     } while (0)
+#define UTTT_Q(PF_)                                                                                                    \
+    do {                                                                                                              \
+        if (res)                                                                                                      \
+            hipLaunchKernelGGL((k_wino3q_conv<true, PF_>), grid, dim3(NTQ), 0, st, x, u, u_scale, bias, res, y, x_amax, \
+                               1, nullptr, nullptr, 0, n_boards);                                                    \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_wino3q_conv<false, PF_>), grid, dim3(NTQ), 0, st, x, u, u_scale, bias, nullptr, y,   \
+                               x_amax, 1, nullptr, nullptr, 0, n_boards);                                            \
+    } while (0)
 #define UTTT_P(PF_, ALA_)                                                                                              \
     do {                                                                                                              \
         if (res)                                                                                                      \
@@ -115,6 +125,9 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
         case 5: UTTT_V(kBufferX | kNoALookahead, 5); break;
         case 6: UTTT_V(kNoALookahead, 3); break;
         case 20: UTTT_V(kFoldBuiltin, 3); break;
+        case 30: UTTT_Q(3); break;
+        case 31: UTTT_Q(2); break;
+        case 32: UTTT_Q(4); break;
         case 22: return uttt_diag_wino3h_scalar(x, u, u_scale, bias, res, y, x_amax, n_boards, stream);
         case 10: UTTT_P(3, true); break;
         case 11: UTTT_P(3, false); break;
@@ -124,6 +137,7 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
     }
 #undef UTTT_V
 #undef UTTT_P
+#undef UTTT_Q
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }
 

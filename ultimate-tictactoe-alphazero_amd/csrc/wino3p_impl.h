@@ -68,18 +68,19 @@ __device__ __forceinline__ floatx2 row_t(const float *__restrict__ xs, int i) {
     else return __builtin_elementwise_fma(mtwo, d(3) - d(1), d(4) - d(2));
 }
 
-template <int B, int A>
+template <int B, int A, bool SCALE = true>
 __device__ __forceinline__ void col_store(const TItem &ti, const TCol &tc) {
     const floatx2 s2 = {ti.sv, ti.sv};
     uint32_t hi, lo;
-    split(tc.o[A] * s2, hi, lo);
+    if constexpr (SCALE) split(tc.o[A] * s2, hi, lo);
+    else split(tc.o[A], hi, lo);
     char *q = ti.vw + (A * 5 + B) * 4 * VPLANE;
     *reinterpret_cast<uint32_t *>(q) = hi;
     *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;
 }
 
 // piece K (0..4) of the transform of column B, spread over the 5 points of a GEMM column
-template <int B, int K>
+template <int B, int K, bool SCALE = true>
 __device__ __forceinline__ void col_piece(const TItem &ti, TCol &tc) {
     if constexpr (K == 0) {
         tc.u[0] = row_t<B>(ti.xs, 0);
@@ -91,23 +92,23 @@ __device__ __forceinline__ void col_piece(const TItem &ti, TCol &tc) {
         tc.u[4] = row_t<B>(ti.xs, 4);
         bt5(tc.u, tc.o);
     } else if constexpr (K == 3) {
-        col_store<B, 0>(ti, tc);
-        col_store<B, 1>(ti, tc);
-        col_store<B, 2>(ti, tc);
+        col_store<B, 0, SCALE>(ti, tc);
+        col_store<B, 1, SCALE>(ti, tc);
+        col_store<B, 2, SCALE>(ti, tc);
     } else {
-        col_store<B, 3>(ti, tc);
-        col_store<B, 4>(ti, tc);
+        col_store<B, 3, SCALE>(ti, tc);
+        col_store<B, 4, SCALE>(ti, tc);
     }
 }
 
-template <int B>
+template <int B, bool SCALE = true>
 __device__ __forceinline__ void col_all(const TItem &ti) {
     TCol tc;
-    col_piece<B, 0>(ti, tc);
-    col_piece<B, 1>(ti, tc);
-    col_piece<B, 2>(ti, tc);
-    col_piece<B, 3>(ti, tc);
-    col_piece<B, 4>(ti, tc);
+    col_piece<B, 0, SCALE>(ti, tc);
+    col_piece<B, 1, SCALE>(ti, tc);
+    col_piece<B, 2, SCALE>(ti, tc);
+    col_piece<B, 3, SCALE>(ti, tc);
+    col_piece<B, 4, SCALE>(ti, tc);
 }
 
 // the whole transform of one chunk (prologue only)
