@@ -4,7 +4,7 @@
 #   train  tools/bench_train.py (eager / HIP graph / graph + channels-last)
 #   cycle  tools/bench_cycle.py (BASELINE configs[4] on one GPU)
 #   hist   tools/bench_history.py (.history path at C4 scale)   vars  conv pipeline variants (diag lib)
-#   bench  bench.py (headline, variants, CPU baselines)     prof  bench under rocprofv3 --kernel-trace --stats
+#   ab     launch-shape A/B (grid policy, lanes, cache size)   bench  bench.py (headline, variants, CPU baselines)     prof  bench under rocprofv3 --kernel-trace --stats
 # Each GPU step has its own time limit; the session stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -27,9 +27,22 @@ for s in $STEPS; do
     tprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tprof -o train \
                -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \
                > $OUT/tprof.log 2>&1 ;;
+    lat)   timeout -k 10 300 python -u tools/diag/latency_single.py > $OUT/latency.log 2>&1 ;;
+    vsmall) VARIANTS= timeout -k 10 300 python -u tools/diag/wino3h_variants.py 250 500 1000 > $OUT/variants_small.log 2>&1 ;;
     tcomp) timeout -k 10 600 python -u tools/diag/train_compare.py > $OUT/train_compare.log 2>&1 ;;
     tcheck) timeout -k 10 300 python -u tools/diag/train_graph_check.py > $OUT/train_check.log 2>&1 ;;
     vars)  timeout -k 10 300 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
+    ab)    # A/B of launch shapes on the headline workload (short runs, one JSON line each)
+           cfgs=("base:" "grid0:UTTT_WINO3H_GRID=0" "grid2:UTTT_WINO3H_GRID=2" "lanes1:--lanes 1"
+                 "lanes1_grid0:UTTT_WINO3H_GRID=0 --lanes 1" "lanes4_grid0:UTTT_WINO3H_GRID=0 --lanes 4" "cache25:--cache-log2 25")
+           [ -n "${AB_CFGS:-}" ] && IFS=';' read -ra cfgs <<< "$AB_CFGS"
+           for cfg in "${cfgs[@]}"; do
+             name=${cfg%%:*}; rest=${cfg#*:}; envs=""; args=""
+             for w in $rest; do case $w in UTTT_*=*) envs="$envs $w" ;; *) args="$args $w" ;; esac; done
+             env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps 10 --warmup 4 $args \
+               > $OUT/ab_$name.log 2>&1 || exit $?
+             echo "$name $(tail -1 $OUT/ab_$name.log | cut -c1-260)" >> $OUT/ab.log
+           done ;;
     bench) timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 ;;
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/prof_bench.log 2>&1 ;;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 
 #include "uttt_nn.h"
@@ -57,6 +58,7 @@ constexpr int kNoALookahead = 1 << 21;  // V fragments read at their own point (
 constexpr int kBufferX = 1 << 22;       // input loads as buffer loads, zero beyond the batch: no branches
 constexpr int kFoldBuiltin = 1 << 23;   // fold as compiler-visible ops (hazards padded by the compiler)
 constexpr int kFoldScalar = 1 << 24;    // ... as scalar v_add_f32 / v_fma_f32 pairs (TU built with -fno-slp-vectorize)
+constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS latency) instead of one
 
 struct Acc {
     floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
@@ -170,7 +172,8 @@ __device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
 // The fold of point XI-1 is issued among point XI's MFMAs.
 template <int XI, int MODE, int PF>
 __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag (&bq)[PF],
-                                        AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff) {
+                                        AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff,
+                                        AFrag *a_next = nullptr) {
     if constexpr (XI <= NP) {
         floatx2 m[4];
         if constexpr (XI < NP) {
@@ -183,8 +186,11 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             }
             const BFrag b0 = bq[0];
             if constexpr (MODE & kNoALookahead) a0 = load_a(sv, XI);  // this point's V, waited for here
-            AFrag a1;
-            if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) {
+            AFrag a1, a2;
+            if constexpr (MODE & kALook2) {  // a_next holds point XI+1 (loaded a point ago); load XI+2
+                if constexpr (XI + 1 < NP) a1 = *a_next;
+                if constexpr (XI + 2 < NP) a2 = load_a(sv, XI + 2);
+            } else if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) {
                 if constexpr (MODE & 16) {  // diagnostic: no A loads
                     a1 = a0;
                     asm volatile("" : "+v"(a1.h0), "+v"(a1.l0), "+v"(a1.h1), "+v"(a1.l1));
@@ -228,12 +234,13 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             for (int i = 0; i + 1 < PF; ++i) bq[i] = bq[i + 1];
             bq[PF - 1] = b2;
             if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) a0 = a1;
+            if constexpr ((MODE & kALook2) && XI + 2 < NP) *a_next = a2;
         }
         if constexpr (XI == NP && !(MODE & 64)) fold_all<XI - 1, MODE>(S, mprev, k2, k4);  // nothing left to spread it over
         if constexpr (XI < NP) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) mprev[i] = m[i];
-            xi_loop<XI + 1, MODE, PF>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff);
+            xi_loop<XI + 1, MODE, PF>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff, a_next);
         }
     }
 }
@@ -280,6 +287,7 @@ __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restric
 
 // Per-board V scales of the SB staged boards of a set (powers of two, uniform over the workgroup)
 struct SetScale {
+    static_assert(SB == 4, "of() selects among exactly four staged boards");
     float s[SB];
     __device__ __forceinline__ float of(int kb) const {
         // a select chain, not a dynamically indexed array (that would live in scratch)
@@ -620,10 +628,11 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         if (g + 1 < G) store_x(sX, xr, sc_next, fresh(tid));
         mark(g, 2, t0);
         if constexpr ((MODE & 3) != 2) {
-            AFrag a0;
+            AFrag a0, an;
             if constexpr (!(MODE & kNoALookahead)) a0 = load_a(sv_lane, 0);
+            if constexpr (MODE & kALook2) an = load_a(sv_lane, 1);
             floatx2 mprev[4];
-            xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff);
+            xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         }
         mark(g, 3, t0);
         if (c == NCH - 1) set_epilogue<RES, MODE>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane);
@@ -634,16 +643,22 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     }
 }
 
+// Workgroups per launch: at most cap sets' worth, cap = CUs x UTTT_WINO3H_GRID (default 1:
+// persistent, a workgroup loops over sets b, b + grid, ...; 0 = one workgroup per set, so the
+// dispatcher hands sets of concurrent launches to whichever CU frees first)
 static int grid_size(int n_boards) {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
+    static int cap = -1;
+    if (cap < 0) {
+        int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             cus <= 0)
             cus = 256;
+        const char *e = getenv("UTTT_WINO3H_GRID");
+        const int k = e && *e ? atoi(e) : 1;
+        cap = k <= 0 ? (1 << 30) : k * cus;
     }
     const int nsets = n_sets(n_boards);
-    return nsets < cus ? nsets : cus;
+    return nsets < cap ? nsets : cap;
 }
 
 }  // namespace wino3h
