@@ -59,6 +59,8 @@ constexpr int kBufferX = 1 << 22;       // input loads as buffer loads, zero bey
 constexpr int kFoldBuiltin = 1 << 23;   // fold as compiler-visible ops (hazards padded by the compiler)
 constexpr int kFoldScalar = 1 << 24;    // ... as scalar v_add_f32 / v_fma_f32 pairs (TU built with -fno-slp-vectorize)
 constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS latency) instead of one
+constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
+constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
 
 struct Acc {
     floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
@@ -330,14 +332,25 @@ __device__ __forceinline__ void bt5(const floatx2 (&d)[5], floatx2 (&t)[5]) {
 }
 
 // (v0, v1) -> packed f16 hi (round to nearest: |v - hi| <= 2^-11 |v|, exact in f32) and
-// f16 lo = the remainder rounded to nearest (v_cvt_pk_f16_f32, one instruction each)
+// f16 lo = the remainder rounded to nearest. hi is one v_cvt_pk_f16_f32. lo is one
+// v_fma_mixlo_f16 + one v_fma_mixhi_f16 (-hi * 1 + v from the f16 half of hi, rounded to
+// f16): v - hi is exact in f32 (Sterbenz), so this equals converting hi back, subtracting and
+// converting (5 instructions and a hazard nop; MIX = false, diagnostics) bit for bit.
+// The compiler folds an fma on a converted half back into that sequence, hence the asm.
 typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+template <bool MIX = true>
 __device__ __forceinline__ void split(floatx2 v, uint32_t &hi, uint32_t &lo) {
     const halfx2 h = __builtin_convertvector(v, halfx2);
-    const floatx2 r = v - __builtin_convertvector(h, floatx2);
-    const halfx2 l = __builtin_convertvector(r, halfx2);
     hi = __builtin_bit_cast(uint32_t, h);
-    lo = __builtin_bit_cast(uint32_t, l);
+    if constexpr (MIX) {
+        uint32_t l;
+        asm volatile("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hi), "v"(v.x));
+        asm volatile("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hi), "v"(v.y));
+        lo = l;
+    } else {
+        const floatx2 r = v - __builtin_convertvector(h, floatx2);
+        lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, halfx2));
+    }
 }
 
 // V = B^T d B for item it = (tile slot lt, channel pair p) of a set that is half h of its
@@ -365,6 +378,7 @@ __device__ __forceinline__ void transform_rows(floatx2 (&uu)[5][5], const float 
     }
 }
 
+template <bool MIX = true>
 __device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floatx2 (&uu)[5][5], int it) {
     const int p = it % (KC / 2), lt = it / (KC / 2);
     // A fragment: lane (row m, kq) holds k = 8kq..8kq+7; channel pair p is k = 2p, 2p+1
@@ -378,7 +392,7 @@ __device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floa
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
             uint32_t hi, lo;
-            split(o[a], hi, lo);
+            split<MIX>(o[a], hi, lo);
             char *q = base + (a * 5 + b) * 4 * VPLANE;
             *reinterpret_cast<uint32_t *>(q) = hi;
             *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;
@@ -386,10 +400,11 @@ __device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floa
     }
 }
 
+template <bool MIX = true>
 __device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it, int h) {
     floatx2 uu[5][5];
     transform_rows(uu, sX, it, h);
-    transform_cols(sv, uu, it);
+    transform_cols<MIX>(sv, uu, it);
 }
 
 // An opaque copy: index math derived from it is recomputed where it is used
@@ -591,20 +606,28 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     // MI355X_MICROARCH.md §LDS); m ^ 4kq made the reads 2-way
     const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (2 * kq)) * 16);
 
-    // zero the pads of sX (never written after this; the staged cells are rewritten every chunk):
-    // the 5 shared zero rows (10 positions each), the zero column of the 36 board rows, the last position
-    for (int i = fresh(tid); i < NPAD * (KC / 4); i += NT) {
-        const int j = i / (KC / 4), q = i % (KC / 4);
-        const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
-                      : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
-        reinterpret_cast<float4 *>(sX + pos * KC)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    // the first chunk's inputs, scales and U fragments are requested before anything else, and the
+    // pads of sX (never written after this; the staged cells are rewritten every chunk) are zeroed
+    // while they are in flight: the 5 shared zero rows (10 positions each), the zero column of the
+    // 36 board rows, the last position. Pads and staged cells are disjoint: one barrier covers both.
+    auto zero_pads = [&]() {
+        for (int i = fresh(tid); i < NPAD * (KC / 4); i += NT) {
+            const int j = i / (KC / 4), q = i % (KC / 4);
+            const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
+                          : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
+            reinterpret_cast<float4 *>(sX + pos * KC)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+    };
+    if constexpr (MODE & kSerialPrologue) {  // diagnostic: the round-2 order (pads, barrier, then loads)
+        zero_pads();
+        __syncthreads();
     }
-    __syncthreads();
+    load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
+    SetScale sc = set_scale(x_amax, x_amax_per_board, set_b0(0), n_boards);  // V scales of the current set
     BFrag bq[PF];
 #pragma unroll
     for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, c_rot, voff);
-    load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
-    SetScale sc = set_scale(x_amax, x_amax_per_board, set_b0(0), n_boards);  // V scales of the current set
+    if constexpr (!(MODE & kSerialPrologue)) zero_pads();
     store_x(sX, xr, sc, tid);
     __syncthreads();
     const bool stamp = (MODE & 4) && blockIdx.x < 64 && (tid == 0 || tid == 256);
@@ -622,7 +645,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         SetScale sc_next = sc;
         if (c == NCH - 1 && g + 1 < G) sc_next = set_scale(x_amax, x_amax_per_board, set_b0(g + 1), n_boards);
         mark(g, 0, t0);
-        if constexpr ((MODE & 3) != 1) transform(sV, sX, fresh(tid), set_of(g) & 1);
+        if constexpr ((MODE & 3) != 1) transform<!(MODE & kSplitCvt)>(sV, sX, fresh(tid), set_of(g) & 1);
         mark(g, 1, t0);
         lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sc_next, fresh(tid));
@@ -643,7 +666,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     }
 }
 
-// Workgroups per launch: at most cap sets' worth, cap = CUs x UTTT_WINO3H_GRID (default 1:
+// Workgroups per launch: at most cap, cap = CUs x UTTT_WINO3H_GRID (a real number, default 1:
 // persistent, a workgroup loops over sets b, b + grid, ...; 0 = one workgroup per set, so the
 // dispatcher hands sets of concurrent launches to whichever CU frees first)
 static int grid_size(int n_boards) {
@@ -654,8 +677,8 @@ static int grid_size(int n_boards) {
             cus <= 0)
             cus = 256;
         const char *e = getenv("UTTT_WINO3H_GRID");
-        const int k = e && *e ? atoi(e) : 1;
-        cap = k <= 0 ? (1 << 30) : k * cus;
+        const double k = e && *e ? atof(e) : 1.0;
+        cap = k <= 0.0 ? (1 << 30) : (int)(k * cus + 0.5) > 0 ? (int)(k * cus + 0.5) : 1;
     }
     const int nsets = n_sets(n_boards);
     return nsets < cap ? nsets : cap;
