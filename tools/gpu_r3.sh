@@ -4,6 +4,7 @@
 #   train  tools/bench_train.py (eager / HIP graph / graph + channels-last)
 #   cycle  tools/bench_cycle.py (BASELINE configs[4] on one GPU)
 #   hist   tools/bench_history.py (.history path at C4 scale)   vars  conv pipeline variants (diag lib)
+#   pmcconv conv HBM traffic (FETCH_SIZE / WRITE_SIZE passes)
 #   ab     launch-shape A/B (grid policy, lanes, cache size)   bench  bench.py (headline, variants, CPU baselines)     prof  bench under rocprofv3 --kernel-trace --stats
 # Each GPU step has its own time limit; the session stops at the first failure.
 set -u
@@ -23,6 +24,8 @@ for s in $STEPS; do
     cycle16) UTTT_TRAIN_PRECISION=f16 timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle_f16.json ${CYCLE_ARGS:-} > $OUT/cycle_f16.log 2>&1 ;;
     hist)  timeout -k 10 300 python -u tools/bench_history.py > $OUT/history.log 2>&1 ;;
     pmcsel) timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 ;;
+    pmcconv) timeout -k 10 600 bash tools/pmc_conv.sh > $OUT/pmc_conv.log 2>&1 && \
+             python tools/pmc_conv_summary.py gpurun_out/pmc_conv ${N:-1344} $OUT/pmc_conv.json >> $OUT/pmc_conv.log 2>&1 ;;
     pmcsq) timeout -k 10 600 bash tools/pmc_sq.sh > $OUT/pmc_sq.log 2>&1 ;;
     tprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tprof -o train \
                -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \
