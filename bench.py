@@ -230,7 +230,7 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
         folded = FoldedDualNetwork(net).to(dev)
         make_inner = lambda eng: NetworkEvaluator(folded, eng.max_trees)  # noqa: E731
     ev_pairs = []
-    rows = [0]
+    rows = []  # per network call: n, or the RoundCount the async round loop fills in
 
     def make_timed(eng):
         inner = make_inner(eng)
@@ -241,10 +241,11 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
             out = inner(x, n)
             b.record()
             ev_pairs.append((a, b))
-            rows[0] += n
+            rows.append(n)
             return out
 
         timed_eval.needs_input = getattr(inner, "needs_input", True)
+        timed_eval.device_count = getattr(inner, "device_count", False)
         return timed_eval
 
     sp.set_evaluator(make_timed)
@@ -253,12 +254,11 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     per_rank = (age + warmup + steps + 2) * games
     gb, ge = shard(per_rank * world, rank, world)
     sp.begin(gb, ge, 1234, arena_plies=per_rank)
-    for _ in range(age + warmup):
-        sp.step()
+    sp.steps(age + warmup)
     torch.cuda.synchronize()
     ev_pairs.clear()
     tower_events.clear()
-    rows[0] = 0
+    rows.clear()
     sp.reset_stats()
     sp.set_timing(True)
     rounds0, finished0 = sp.rounds, sp.finished
@@ -268,19 +268,18 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     base = torch.cuda.Event(enable_timing=True)
     base.record()
     t0 = time.perf_counter()
-    done = 0
-    for _ in range(steps):
-        done += sp.step()
+    done = sp.steps(steps)  # every lane plays `steps` moves (lanes pipelined across moves)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     torch.cuda.synchronize()
     ivs = [(base.elapsed_time(a), base.elapsed_time(b)) for a, b in ev_pairs]
-    tower = [(n, a.elapsed_time(b)) for n, a, b in tower_events]
+    # rounds enqueued before their count was known may have had no leaf (the move's last select)
+    tower = [(int(n), a.elapsed_time(b)) for n, a, b in tower_events if int(n) > 0]
     st = {k: sp.kernel_stats(k) for k in ("select", "apply", "scan", "move_end", "select_levels", "select_trees",
                                           "select_max_levels_sum")}
-    out = {"sims": done, "elapsed": elapsed, "rows": rows[0], "nn_ms": union_ms(ivs),
+    out = {"sims": done, "elapsed": elapsed, "rows": sum(int(n) for n in rows), "nn_ms": union_ms(ivs),
            "nn_lane_sum_ms": sum(hi - lo for lo, hi in ivs), "tower": tower, "stats": st,
            "rounds": sp.rounds - rounds0, "finished": sp.finished - finished0, "conv": conv,
            "cache": sp.cache_stats() if cache_log2 else None, "trees_per_launch": games // lanes}

@@ -131,6 +131,20 @@ int uttt_search_begin_mode(uttt_engine_t *eng, const uttt_state_t *roots, int32_
  * the stream to read the count. */
 int uttt_search_select(uttt_engine_t *eng, float *nn_input, int32_t *n_pending);
 
+/* The same round without reading the count on the host: launches the descents and the
+ * pending-leaf scan and returns at once. The count stays on the device (uttt_search_count_ptr:
+ * [0] pending leaves, [1] trees stopped by the select budget); uttt_nn_stem, the *_dev network
+ * entry points and uttt_search_apply (device results, one row per leaf) read it there, so a
+ * round is enqueued with no host synchronisation. A round whose count is 0 changes nothing:
+ * the caller enqueues rounds until a count it copied back (uttt_search_count_copy) reads
+ * [0] == 0 and [1] == 0, the point where uttt_search_select would report 0. Replaces the
+ * per-round blocking read of uttt_search_select for the self-play driver. */
+int uttt_search_select_async(uttt_engine_t *eng);
+/* Enqueue a copy of the round's two counts to dst (host, pinned for an asynchronous copy). */
+int uttt_search_count_copy(uttt_engine_t *eng, int32_t *dst);
+/* Device address of the round's two counts. */
+int uttt_search_count_ptr(uttt_engine_t *eng, const int32_t **count);
+
 /* Host copies of the pending leaves (slot order) and their multiplicity k
  * (the number of identical copies the reference would have queued). */
 int uttt_search_pending(uttt_engine_t *eng, uttt_state_t *states, int32_t *copies);

@@ -32,7 +32,8 @@ extern "C" {
 #define UTTT_HEAD_VFC2_B (UTTT_HEAD_VFC2_W + 256)
 #define UTTT_HEAD_SIZE (UTTT_HEAD_VFC2_B + 1)
 
-/* Stem from the engine's pending leaves (slot order, after uttt_search_select):
+/* Stem from the engine's pending leaves (slot order, after uttt_search_select, or after
+ * uttt_search_select_async with the count read on the device):
  * out[n][81][128] = relu(conv3x3(planes, w) + b) with w[27][128] = folded
  * conv_input weight laid out [in_plane*9 + ky*3 + kx][out_channel]
  * (dual_network.py:89-92; planes of uttt_game.cpp:244-280). Engine stream. */
@@ -45,6 +46,10 @@ int uttt_nn_stem_states(const uttt_state_t *states, int32_t n, const float *w, c
  * activation (n,81,128) (dual_network.py:106-121). */
 int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float *policy, float *value,
                   int32_t softmax, void *stream);
+/* The same for a device-resident count *n_dev <= max_n (uttt_search_select_async): the grid is
+ * sized for max_n and rows past *n_dev are not touched. */
+int uttt_nn_heads_dev(const float *act, const float *head_weights, const int32_t *n_dev, int32_t max_n,
+                      float *policy, float *value, int32_t softmax, void *stream);
 
 /* Residual-tower 3x3 conv (128->128, pad 1, 9x9 boards) + bias (+ residual) + ReLU as one
  * Winograd F(3x3,3x3) kernel (csrc/wino3h_conv.hip; dual_network.py:28-45): a 9x9 board is
@@ -66,6 +71,11 @@ int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, con
                            const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
                            uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, int32_t n_boards,
                            void *stream);
+/* The same conv on min(*n_dev, max_boards) boards, the count read on the device. */
+int uttt_nn_conv3x3_wino3h_dev(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                               const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                               uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
+                               int32_t max_boards, void *stream);
 /* *amax = max(*amax, max |x[i]|) over count floats, as u32 float bits (zero *amax first). */
 int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream);
 

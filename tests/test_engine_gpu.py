@@ -403,18 +403,23 @@ def test_fused_selfplay_lanes_are_bit_identical(gpu):
     1 lane without the evaluation cache, 1 lane with it, and 2 lanes sharing it (two
     engines on two streams, network calls overlapping) give the same records bit for
     bit - every kernel computes a board independently of the batch it is in, so cached
-    outputs equal fresh ones."""
+    outputs equal fresh ones. The rounds run without a per-round host sync (the count read
+    on the device, SelfPlay._rounds_async) except in the last configuration, the blocking
+    loop: same records and the same number of network rounds."""
     from uttt_amd.model import calibrated_network
     from uttt_amd.nnfast import FusedNetworkEvaluator
     net = calibrated_network(NETCAL, "cuda")
-    out = []
-    for lanes, cache in ((1, 0), (1, 16), (2, 16)):
+    out, rounds = [], []
+    for lanes, cache, asy in ((1, 0, True), (1, 16, True), (2, 16, True), (2, 16, False)):
         sp = gpu.SelfPlay(16, 50, 8, 1.0, lanes=lanes, cache_log2=cache)
+        sp.async_rounds = asy
         sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng))
         sp.run(0, 12, 4321)
         out.append(sp.records())
+        rounds.append(sp.rounds)
         if cache:
             assert sp.cache_stats()["hits"] > 0
+    assert rounds[2] == rounds[3]
     a = out[0]
     for b in out[1:]:
         assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(12))

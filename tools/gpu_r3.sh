@@ -26,6 +26,8 @@ for s in $STEPS; do
     pmcsel) timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 ;;
     pmcconv) timeout -k 10 600 bash tools/pmc_conv.sh > $OUT/pmc_conv.log 2>&1 && \
              python tools/pmc_conv_summary.py gpurun_out/pmc_conv ${N:-1344} $OUT/pmc_conv.json >> $OUT/pmc_conv.log 2>&1 ;;
+    pmcl2) timeout -k 10 1000 bash tools/pmc_l2.sh > $OUT/pmc_l2.log 2>&1 && \
+           python tools/pmc_l2_summary.py gpurun_out/pmc_l2 ${NB:-1381} $OUT/pmc_l2.json >> $OUT/pmc_l2.log 2>&1 ;;
     pmcsq) timeout -k 10 600 bash tools/pmc_sq.sh > $OUT/pmc_sq.log 2>&1 ;;
     tprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tprof -o train \
                -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \

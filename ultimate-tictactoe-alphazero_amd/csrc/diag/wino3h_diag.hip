@@ -20,7 +20,7 @@ static void ablation_res(const float *x, const uint16_t *u, float u_scale, const
                          const uint32_t *x_amax, int32_t n_boards, hipStream_t st) {
     using namespace wino3h;
     hipLaunchKernelGGL((k_wino3h_conv<true, MODE>), dim3(grid_size(n_boards)), dim3(NT), 0, st, x, u, u_scale, bias,
-                       g_diag_res ? g_diag_res : x, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+                       g_diag_res ? g_diag_res : x, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);
 }
 
 extern "C" {
@@ -48,29 +48,29 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
         return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
     }
     switch (mode) {
-        case 131072: hipLaunchKernelGGL((k_wino3h_conv<false, 131072>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 16: hipLaunchKernelGGL((k_wino3h_conv<false, 16>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 32: hipLaunchKernelGGL((k_wino3h_conv<false, 32>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 48: hipLaunchKernelGGL((k_wino3h_conv<false, 48>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 68: hipLaunchKernelGGL((k_wino3h_conv<false, 68>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 116: hipLaunchKernelGGL((k_wino3h_conv<false, 116>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 20: hipLaunchKernelGGL((k_wino3h_conv<false, 20>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 8192: hipLaunchKernelGGL((k_wino3h_conv<false, 8192>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 8196: hipLaunchKernelGGL((k_wino3h_conv<false, 8196>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 260: hipLaunchKernelGGL((k_wino3h_conv<false, 260>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+        case 131072: hipLaunchKernelGGL((k_wino3h_conv<false, 131072>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 1: hipLaunchKernelGGL((k_wino3h_conv<false, 1>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 2: hipLaunchKernelGGL((k_wino3h_conv<false, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 64: hipLaunchKernelGGL((k_wino3h_conv<false, 64>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 16: hipLaunchKernelGGL((k_wino3h_conv<false, 16>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 32: hipLaunchKernelGGL((k_wino3h_conv<false, 32>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 48: hipLaunchKernelGGL((k_wino3h_conv<false, 48>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 36: hipLaunchKernelGGL((k_wino3h_conv<false, 36>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 68: hipLaunchKernelGGL((k_wino3h_conv<false, 68>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 116: hipLaunchKernelGGL((k_wino3h_conv<false, 116>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 20: hipLaunchKernelGGL((k_wino3h_conv<false, 20>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 512: hipLaunchKernelGGL((k_wino3h_conv<false, 512>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 8192: hipLaunchKernelGGL((k_wino3h_conv<false, 8192>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 8196: hipLaunchKernelGGL((k_wino3h_conv<false, 8196>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 260: hipLaunchKernelGGL((k_wino3h_conv<false, 260>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 65: hipLaunchKernelGGL((k_wino3h_conv<false, 65>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);
     }
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }
@@ -94,10 +94,10 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
     do {                                                                                                              \
         if (res)                                                                                                      \
             hipLaunchKernelGGL((k_wino3h_conv<true, M, P>), grid, dim3(NT), 0, st, x, u, u_scale, bias, res, y, x_amax, \
-                               1, nullptr, nullptr, 0, n_boards);                                                    \
+                               1, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);                                                    \
         else                                                                                                          \
             hipLaunchKernelGGL((k_wino3h_conv<false, M, P>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y,   \
-                               x_amax, 1, nullptr, nullptr, 0, n_boards);                                            \
+                               x_amax, 1, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);                                            \
     } while (0)
 #define UTTT_Q(PF_)                                                                                                    \
     do {                                                                                                              \
@@ -153,11 +153,11 @@ int uttt_diag_wino3h_pf(const float *x, const uint16_t *u, float u_scale, const 
     hipStream_t st = (hipStream_t)stream;
     using namespace wino3h;
     switch (pf) {
-        case 3: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 6: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 6>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards); break;
-        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards);
+        case 3: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 6: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 6>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        default: hipLaunchKernelGGL((k_wino3h_conv<false, 0, 2>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);
     }
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }

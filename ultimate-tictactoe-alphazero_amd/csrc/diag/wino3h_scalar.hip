@@ -20,9 +20,9 @@ extern "C" int uttt_diag_wino3h_scalar(const float *x, const uint16_t *u, float 
     hipStream_t st = (hipStream_t)stream;
     if (res)
         hipLaunchKernelGGL((k_wino3h_conv<true, kFoldScalar, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias, res, y,
-                           x_amax, 1, nullptr, nullptr, 0, n_boards);
+                           x_amax, 1, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);
     else
         hipLaunchKernelGGL((k_wino3h_conv<false, kFoldScalar, 3>), grid, dim3(NT), 0, st, x, u, u_scale, bias,
-                           nullptr, y, x_amax, 1, nullptr, nullptr, 0, n_boards);
+                           nullptr, y, x_amax, 1, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }

@@ -1228,7 +1228,8 @@ struct uttt_engine {
     int32_t *d_visits = nullptr;
     int64_t bytes = 0;
     // round state
-    int phase = 0;  // 0 idle, 1 search begun (select next), 2 selected (apply next)
+    int phase = 0;  // 0 idle, 1 search begun (select next), 2 selected (apply next),
+                    // 3 selected without reading the count (uttt_search_select_async; apply next)
     int n_pending = 0;
     bool selfplay = false;
     // self-play
@@ -1349,16 +1350,20 @@ int ensure_scratch(uttt_engine *e, int64_t rows) {
 
 namespace uttt {
 // For the evaluator kernels (nn_kernels.hip): the pending leaves of the current round.
+// After uttt_search_select_async the count is on the device only: *n = -1, *n_dev points at
+// it and *max_n bounds it (launch grids sized for max_n, kernels exit past *n_dev).
 int engine_pending_view(uttt_engine_t *e, const uttt_state_t **leaf, const int32_t **tree_of, int32_t *n,
-                        hipStream_t *stream) {
+                        const int32_t **n_dev, int32_t *max_n, hipStream_t *stream) {
     if (!e) return UTTT_ERR_ARG;
-    if (e->phase != 2) {
+    if (e->phase != 2 && e->phase != 3) {
         set_error("no pending leaves (call uttt_search_select first)");
         return UTTT_ERR_ORDER;
     }
     *leaf = e->tr.leaf;
     *tree_of = e->tr.tree_of;
-    *n = e->n_pending;
+    *n = e->phase == 2 ? e->n_pending : -1;
+    *n_dev = e->phase == 3 ? e->tr.count : nullptr;
+    *max_n = e->tr.n_trees;
     *stream = e->stream;
     return UTTT_OK;
 }
@@ -1550,6 +1555,43 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     return UTTT_OK;
 }
 
+int uttt_search_select_async(uttt_engine_t *e) {
+    if (!e) return UTTT_ERR_ARG;
+    if (e->phase != 1) {
+        set_error("uttt_search_select_async: call uttt_search_begin (or apply the previous round) first");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = 0;
+    {
+        TimedLaunch tl(e, kKSelect);
+        hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+                           e->cache, e->timing ? e->d_bytes : nullptr);
+    }
+    if ((rc = check_launch())) return rc;
+    {
+        TimedLaunch tl(e, kKScan);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr);
+    }
+    if ((rc = check_launch())) return rc;
+    e->n_pending = -1;
+    e->phase = 3;
+    return UTTT_OK;
+}
+
+int uttt_search_count_copy(uttt_engine_t *e, int32_t *dst) {
+    if (!e || !dst) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpyAsync(dst, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    return UTTT_OK;
+}
+
+int uttt_search_count_ptr(uttt_engine_t *e, const int32_t **count) {
+    if (!e || !count) return UTTT_ERR_ARG;
+    *count = e->tr.count;
+    return UTTT_OK;
+}
+
 int uttt_search_pending(uttt_engine_t *e, uttt_state_t *states, int32_t *copies) {
     if (!e) return UTTT_ERR_ARG;
     if (e->phase != 2) {
@@ -1579,8 +1621,12 @@ int uttt_search_apply(uttt_engine_t *e, const float *policy, int64_t pld, const 
         set_error("uttt_search_apply: bad arguments (policy stride must be >= 81)");
         return UTTT_ERR_ARG;
     }
-    if (e->phase != 2) {
+    if (e->phase != 2 && e->phase != 3) {
         set_error("uttt_search_apply: no pending leaves (call uttt_search_select)");
+        return UTTT_ERR_ORDER;
+    }
+    if (e->phase == 3 && (per_copy || !on_device)) {
+        set_error("uttt_search_apply: after uttt_search_select_async the results must be on the device, one per leaf");
         return UTTT_ERR_ORDER;
     }
     if (per_copy && e->tr.py) {
@@ -1588,7 +1634,8 @@ int uttt_search_apply(uttt_engine_t *e, const float *policy, int64_t pld, const 
         return UTTT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(e->device));
-    const int n = e->n_pending;
+    // phase 3: the count is on the device; k_apply reads it (tr.count[0]) and the grid covers every tree
+    const int n = e->phase == 3 ? e->tr.n_trees : e->n_pending;
     const int32_t *rowbase = nullptr;
     int64_t rows = n;
     if (per_copy) {
@@ -1789,7 +1836,7 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
         set_error("uttt_selfplay_move_end: call uttt_selfplay_begin first");
         return UTTT_ERR_ORDER;
     }
-    if (e->phase == 2) {
+    if (e->phase == 2 || e->phase == 3) {
         set_error("uttt_selfplay_move_end: pending leaves were not applied");
         return UTTT_ERR_ORDER;
     }

@@ -18,7 +18,7 @@ namespace uttt {
 
 void set_error(const char *fmt, ...);
 int engine_pending_view(uttt_engine_t *e, const uttt_state_t **leaf, const int32_t **tree_of, int32_t *n,
-                        hipStream_t *stream);
+                        const int32_t **n_dev, int32_t *max_n, hipStream_t *stream);
 
 namespace nn {
 
@@ -37,11 +37,13 @@ __device__ __forceinline__ uint32_t bit3(uint32_t w0, uint32_t w1, uint32_t w2, 
     return (w >> (a % 27)) & 1u;
 }
 __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ leaf, const int32_t *__restrict__ tree_of,
-                                              int n, const float *__restrict__ w, const float *__restrict__ b,
-                                              float *__restrict__ out) {
+                                              int n, const int32_t *__restrict__ n_dev, const float *__restrict__ w,
+                                              const float *__restrict__ b, float *__restrict__ out) {
     __shared__ float4 s_w[27 * (C / 4)];
     __shared__ uint32_t s_mask[SB * 81];
     const int s0 = blockIdx.x * SB;
+    if (n_dev) n = min(n, *n_dev);  // the count k_scan left on the device (grid sized for the maximum n)
+    if (s0 >= n) return;
     const int nb = n - s0 < SB ? n - s0 : SB;
     const int t = threadIdx.x;
     for (int i = t; i < 27 * (C / 4); i += 256) s_w[i] = reinterpret_cast<const float4 *>(w)[i];
@@ -93,12 +95,15 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
 // take 120 / 73 / 60 / 53 / 52 us at HB = 16 / 8 / 4 / 2 / 1 (tools/diag/nn_parts.py).
 constexpr int HB = 1;
 __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, const float *__restrict__ hw, int n,
-                                               float *__restrict__ policy, float *__restrict__ value, int softmax) {
+                                               const int32_t *__restrict__ n_dev, float *__restrict__ policy,
+                                               float *__restrict__ value, int softmax) {
     __shared__ float s_h[HB][3 * 81];  // relu(1x1 conv): [p0 | p1 | v] x 81 (NCHW flatten order)
     __shared__ float s_z[HB][81];      // policy logits
     __shared__ float s_v[HB][4];       // value FC2 partial sums, one per wave
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int b0 = blockIdx.x * HB;
+    if (n_dev) n = min(n, *n_dev);
+    if (b0 >= n) return;
     const int nb = n - b0 < HB ? n - b0 : HB;
     // 1x1 convs (128 -> 2 policy planes, 128 -> 1 value plane) + ReLU: 16 lanes per
     // (position, board), 8 channels per lane, 16-lane shuffle reduction
@@ -215,17 +220,19 @@ extern "C" {
 
 int uttt_nn_stem(uttt_engine_t *e, const float *w, const float *b, float *out) {
     const uttt_state_t *leaf;
-    const int32_t *tree_of;
-    int32_t n;
+    const int32_t *tree_of, *n_dev;
+    int32_t n, max_n;
     hipStream_t st;
-    int rc = engine_pending_view(e, &leaf, &tree_of, &n, &st);
+    int rc = engine_pending_view(e, &leaf, &tree_of, &n, &n_dev, &max_n, &st);
     if (rc) return rc;
     if (!w || !b || !out) {
         set_error("uttt_nn_stem: null pointer");
         return UTTT_ERR_ARG;
     }
+    if (n_dev) n = max_n;  // count on the device: grid for every tree, the kernel reads the count
     if (n == 0) return UTTT_OK;
-    hipLaunchKernelGGL(nn::k_stem, dim3((n + nn::SB - 1) / nn::SB), dim3(256), 0, st, leaf, tree_of, n, w, b, out);
+    hipLaunchKernelGGL(nn::k_stem, dim3((n + nn::SB - 1) / nn::SB), dim3(256), 0, st, leaf, tree_of, n, n_dev, w, b,
+                       out);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_stem launch: %s", hipGetErrorString(r));
@@ -242,7 +249,7 @@ int uttt_nn_stem_states(const uttt_state_t *states, int32_t n, const float *w, c
     }
     if (n == 0) return UTTT_OK;
     hipLaunchKernelGGL(nn::k_stem, dim3((n + nn::SB - 1) / nn::SB), dim3(256), 0, (hipStream_t)stream, states, nullptr, n,
-                       w, b, out);
+                       (const int32_t *)nullptr, w, b, out);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_stem launch: %s", hipGetErrorString(r));
@@ -258,8 +265,25 @@ int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float 
         return UTTT_ERR_ARG;
     }
     if (n == 0) return UTTT_OK;
-    hipLaunchKernelGGL(nn::k_heads, dim3((n + nn::HB - 1) / nn::HB), dim3(256), 0, (hipStream_t)stream, act, head_weights, n, policy, value,
-                       softmax ? 1 : 0);
+    hipLaunchKernelGGL(nn::k_heads, dim3((n + nn::HB - 1) / nn::HB), dim3(256), 0, (hipStream_t)stream, act, head_weights, n,
+                       (const int32_t *)nullptr, policy, value, softmax ? 1 : 0);
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) {
+        set_error("k_heads launch: %s", hipGetErrorString(r));
+        return UTTT_ERR_HIP;
+    }
+    return UTTT_OK;
+}
+
+int uttt_nn_heads_dev(const float *act, const float *head_weights, const int32_t *n_dev, int32_t max_n, float *policy,
+                      float *value, int32_t softmax, void *stream) {
+    if (!act || !head_weights || !n_dev || !policy || !value || max_n < 0) {
+        set_error("uttt_nn_heads_dev: bad arguments");
+        return UTTT_ERR_ARG;
+    }
+    if (max_n == 0) return UTTT_OK;
+    hipLaunchKernelGGL(nn::k_heads, dim3((max_n + nn::HB - 1) / nn::HB), dim3(256), 0, (hipStream_t)stream, act,
+                       head_weights, max_n, n_dev, policy, value, softmax ? 1 : 0);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_heads launch: %s", hipGetErrorString(r));

@@ -130,9 +130,10 @@ int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale) {
     return UTTT_OK;
 }
 
-int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *residual,
-                           float *y, const uint32_t *x_amax, int32_t x_amax_per_board, uint32_t *y_amax,
-                           uint32_t *amax_clear, int32_t clear_count, int32_t n_boards, void *stream) {
+static int conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *residual,
+                          float *y, const uint32_t *x_amax, int32_t x_amax_per_board, uint32_t *y_amax,
+                          uint32_t *amax_clear, int32_t clear_count, int32_t n_boards, const int32_t *n_dev,
+                          void *stream) {
     if (!x || !u || !bias || !y || !x_amax || n_boards < 0 || x == y || (residual && residual == y) ||
         !(u_scale > 0.0f) || clear_count < 0 || (clear_count > 0 && !amax_clear) ||
         (amax_clear && (amax_clear == y_amax || amax_clear == x_amax))) {
@@ -145,16 +146,35 @@ int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, con
     const int pb = x_amax_per_board ? 1 : 0;
     if (residual)
         hipLaunchKernelGGL(wino3h::k_wino3h_conv<true>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
-                           bias, residual, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards);
+                           bias, residual, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
     else
         hipLaunchKernelGGL(wino3h::k_wino3h_conv<false>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
-                           bias, nullptr, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards);
+                           bias, nullptr, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_wino3h_conv launch: %s", hipGetErrorString(r));
         return UTTT_ERR_HIP;
     }
     return UTTT_OK;
+}
+
+int uttt_nn_conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *residual,
+                           float *y, const uint32_t *x_amax, int32_t x_amax_per_board, uint32_t *y_amax,
+                           uint32_t *amax_clear, int32_t clear_count, int32_t n_boards, void *stream) {
+    return conv3x3_wino3h(x, u, u_scale, bias, residual, y, x_amax, x_amax_per_board, y_amax, amax_clear, clear_count,
+                          n_boards, nullptr, stream);
+}
+
+int uttt_nn_conv3x3_wino3h_dev(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                               const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                               uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
+                               int32_t max_boards, void *stream) {
+    if (!n_dev) {
+        set_error("uttt_nn_conv3x3_wino3h_dev: n_dev required");
+        return UTTT_ERR_ARG;
+    }
+    return conv3x3_wino3h(x, u, u_scale, bias, residual, y, x_amax, x_amax_per_board, y_amax, amax_clear, clear_count,
+                          max_boards, n_dev, stream);
 }
 
 int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream) {

@@ -565,7 +565,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                                                     const float *__restrict__ res, float *__restrict__ y,
                                                     const uint32_t *__restrict__ x_amax, int x_amax_per_board,
                                                     uint32_t *__restrict__ y_amax, uint32_t *__restrict__ amax_clear,
-                                                    int clear_count, int n_boards) {
+                                                    int clear_count, int n_boards, const int32_t *__restrict__ n_dev) {
     // sX [padded position][channel] (border = 0) then sV
     __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
     float *const sX = reinterpret_cast<float *>(smem);
@@ -573,6 +573,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     // zero the per-board max row a later conv of this forward accumulates into
     for (int i = (int)blockIdx.x * NT + tid; i < clear_count; i += (int)gridDim.x * NT) amax_clear[i] = 0u;
+    // a device-resident board count (the engine's pending count): the grid was sized for n_boards
+    if (n_dev) n_boards = min(n_boards, *n_dev);
     const int nsets = n_sets(n_boards);
     if ((int)blockIdx.x >= nsets) return;
     const int my_sets = (nsets - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;

@@ -68,6 +68,9 @@ SIGNATURES = {
     "uttt_search_begin": (ctypes.c_int, [_P, _SP, _I32, _I32, _I32]),
     "uttt_search_begin_mode": (ctypes.c_int, [_P, _SP, _I32, _I32, _I32, _I32]),
     "uttt_search_select": (ctypes.c_int, [_P, _P, _I32P]),
+    "uttt_search_select_async": (ctypes.c_int, [_P]),
+    "uttt_search_count_copy": (ctypes.c_int, [_P, _P]),
+    "uttt_search_count_ptr": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     "uttt_search_pending": (ctypes.c_int, [_P, _SP, _I32P]),
     "uttt_search_apply": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _I32, _I32]),
     "uttt_eval_hash": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
@@ -91,8 +94,11 @@ SIGNATURES = {
     "uttt_nn_stem": (ctypes.c_int, [_P, _P, _P, _P]),
     "uttt_nn_stem_states": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P]),
     "uttt_nn_heads": (ctypes.c_int, [_P, _P, _I32, _P, _P, _I32, _P]),
+    "uttt_nn_heads_dev": (ctypes.c_int, [_P, _P, _P, _I32, _P, _P, _I32, _P]),
     "uttt_nn_wino3h_weights": (ctypes.c_int, [_F32P, _P, ctypes.POINTER(ctypes.c_float)]),
     "uttt_nn_conv3x3_wino3h": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, _P, _P, _P, _I32, _P, _P, _I32, _I32, _P]),
+    "uttt_nn_conv3x3_wino3h_dev": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, _P, _P, _P, _I32, _P, _P, _I32, _P, _I32,
+                                                  _P]),
     "uttt_nn_amax": (ctypes.c_int, [_P, _I64, _P, _P]),
 }
 

@@ -30,6 +30,23 @@ def initial_states(n):
     return out
 
 
+class RoundCount:
+    """The pending-leaf count of a round enqueued with Engine.select_async: None until the
+    host has read the copy back (SelfPlay fills it), then an int (int(rc) works from then on).
+    Passed to a device-count evaluator in place of n."""
+    __slots__ = ("n",)
+
+    def __init__(self):
+        self.n = None
+
+    def __int__(self):
+        if self.n is None:
+            raise RuntimeError("round count not read back yet")
+        return self.n
+
+    __index__ = __int__
+
+
 class Engine:
     def __init__(self, max_trees, max_sims=50, device=None):
         import torch
@@ -96,6 +113,22 @@ class Engine:
         check(self.lib.uttt_search_select(self.h, p, ctypes.byref(n)))
         self.n_pending = n.value
         return n.value
+
+    def select_async(self):
+        """One round with the pending count left on the device (uttt_search_select_async): the
+        network's *_dev entry points and apply() read it there; count_copy() fetches it."""
+        check(self.lib.uttt_search_select_async(self.h))
+        self.n_pending = None
+
+    def count_copy(self, dst):
+        """Enqueue a copy of the round's [pending, stopped] counts into dst (pinned int32 host tensor)."""
+        check(self.lib.uttt_search_count_copy(self.h, ctypes.c_void_p(dst.data_ptr())))
+
+    def count_ptr(self):
+        """Device address of the round's [pending, stopped] counts."""
+        p = ctypes.c_void_p()
+        check(self.lib.uttt_search_count_ptr(self.h, ctypes.byref(p)))
+        return p
 
     def pending(self):
         n = self.n_pending

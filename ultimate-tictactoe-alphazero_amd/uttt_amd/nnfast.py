@@ -21,6 +21,7 @@ import torch
 
 from . import _lib
 from ._lib import check
+from .engine import RoundCount
 from .model import fold_bn
 
 HEAD = {}
@@ -96,8 +97,11 @@ def _prepared_weights(net, dev, conv):
 
 class FusedNetworkEvaluator:
     """Leaf evaluator over an engine's pending leaves (needs_input = False: the stem reads
-    the leaves' bitboards, the engine never builds the NCHW tensor)."""
+    the leaves' bitboards, the engine never builds the NCHW tensor). device_count: called
+    with a RoundCount (after Engine.select_async) it reads the leaf count on the device, so
+    the round needs no host synchronisation."""
     needs_input = False
+    device_count = True
     NROW = 4  # per-board max rows, rotated over the 32 convs (see __init__, _tower_heads)
 
     def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None):
@@ -142,8 +146,12 @@ class FusedNetworkEvaluator:
 
     @torch.no_grad()
     def forward(self, n, softmax=True):
-        """Evaluate the engine's n pending leaves; returns (policy or logits (n,81), value (n,))."""
+        """Evaluate the engine's n pending leaves; returns (policy or logits (n,81), value (n,)).
+        n a RoundCount: the count is read on the device (Engine.select_async), and the full
+        (max_batch, 81) / (max_batch,) buffers are returned (rows past the count untouched)."""
         check(self.lib.uttt_nn_stem(self.engine.h, _p(self.stem_w), _p(self.stem_b), _p(self.buf[0])))
+        if isinstance(n, RoundCount):
+            return self._tower_heads(n, softmax, n_dev=self.engine.count_ptr())
         return self._tower_heads(n, softmax)
 
     @torch.no_grad()
@@ -163,31 +171,40 @@ class FusedNetworkEvaluator:
                                            self._stream()))
         return self._tower_heads(n, softmax)
 
-    def _tower_heads(self, n, softmax):
+    def _tower_heads(self, n, softmax, n_dev=None):
         stream = self._stream()
         x, t, y = self.buf
         if self.tower_events is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-        fn = self.lib.uttt_nn_conv3x3_wino3h
         rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
         cap = self.max_batch
+        if n_dev is None:
+            fn = self.lib.uttt_nn_conv3x3_wino3h
+            count = (n,)
+        else:  # the count on the device, grids sized for max_batch
+            fn = self.lib.uttt_nn_conv3x3_wino3h_dev
+            count = (n_dev, cap)
         i = 0
         for (u1, s1, b1), (u2, s2, b2) in self.wino:
             src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
             check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), src[0], src[1], rows[i % 4],
-                     rows[(i + 1) % 4], cap, n, stream))
+                     rows[(i + 1) % 4], cap, *count, stream))
             i += 1
             check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), rows[(i - 1) % 4], 1, rows[i % 4],
-                     rows[(i + 1) % 4], cap, n, stream))
+                     rows[(i + 1) % 4], cap, *count, stream))
             i += 1
             x, y = y, x
         if self.tower_events is not None:
             ev1.record()
             self.tower_events.append((n, ev0, ev1))
-        check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
-                                     1 if softmax else 0, stream))
-        return self.policy[:n], self.value[:n]
+        if n_dev is None:
+            check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
+                                         1 if softmax else 0, stream))
+            return self.policy[:n], self.value[:n]
+        check(self.lib.uttt_nn_heads_dev(_p(x), _p(self.heads), n_dev, cap, _p(self.policy), _p(self.value),
+                                         1 if softmax else 0, stream))
+        return self.policy, self.value
 
     def __call__(self, x, n):
         return self.forward(n, True)

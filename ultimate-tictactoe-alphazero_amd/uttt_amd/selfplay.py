@@ -8,12 +8,13 @@ every live tree contributes its one pending leaf to a single network batch.
 import collections
 import contextlib
 import math
+import os
 import time
 
 import numpy as np
 import torch
 
-from .engine import Engine, initial_states
+from .engine import Engine, RoundCount, initial_states
 
 
 def _bucket(n, cap, quantum=256):
@@ -109,6 +110,7 @@ class _Lane:
         self.evaluator = None
         self.rounds = 0
         self.finished = 0
+        self.count_host = None  # pinned [pending, stopped] of the round in flight (async rounds)
 
     def use_stream(self):
         self.engine.use_stream(self.stream)
@@ -154,6 +156,9 @@ class SelfPlay:
             self.evaluator = evaluator
         self.sims = 0
         self.moves = 0
+        # rounds without a per-round host sync when every lane's evaluator reads the count on
+        # the device (FusedNetworkEvaluator); UTTT_ASYNC_ROUNDS=0 keeps the blocking loop
+        self.async_rounds = os.environ.get("UTTT_ASYNC_ROUNDS", "1") != "0"
 
     # one evaluator object per lane (each owns its buffers); with one lane the
     # attribute form is kept for compatibility
@@ -201,8 +206,13 @@ class SelfPlay:
             ln.rounds = ln.finished = 0
         self.sims = self.moves = 0
 
+    def _device_count(self):
+        return self.async_rounds and all(getattr(ln.evaluator, "device_count", False) for ln in self.lanes)
+
     def step(self):
         """One move for every live game. Returns the simulations it ran (0 = all games over)."""
+        if self._device_count():
+            return self.steps(1)
         live = []
         for ln in self.lanes:
             with self._ctx(ln):
@@ -231,12 +241,92 @@ class SelfPlay:
         self.sims += done
         return done
 
+    def steps(self, k=None, progress=None):
+        """k moves of every lane (None: until every lane's games are over); returns the
+        simulations run. With device-count evaluators (FusedNetworkEvaluator) the lanes are
+        pipelined. A round's select, network and apply are enqueued without a host sync (the
+        pending count stays on the device, Engine.select_async), and the host reads each round's
+        count back - a pinned copy right after the select's scan - only to decide whether to
+        enqueue the next round, while the current round's network still runs; so each lane's
+        stream always holds work. A lane begins its next move as soon as its own move ends, so
+        no lane idles at a move boundary while the other finishes. The sequence of select
+        launches per lane equals the blocking loop's (a round without pending leaves changes
+        nothing), each game depends only on its id, and every lane plays exactly k moves:
+        records and totals are those of k lockstep steps (UTTT_ASYNC_ROUNDS=0)."""
+        if not self._device_count():
+            total, i = 0, 0
+            while k is None or i < k:
+                d = self.step()
+                if d == 0:
+                    break
+                total += d
+                i += 1
+                if progress:
+                    progress(self.finished, None)
+            return total
+        for ln in self.lanes:
+            if ln.count_host is None:
+                ln.count_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+
+        def begin_move(ln):
+            with self._ctx(ln):
+                return ln.engine.move_begin()
+
+        state = {}
+        for ln in self.lanes:
+            live = begin_move(ln)
+            if live > 0:
+                state[id(ln)] = [ln, k, live, self._enqueue_round(ln)]
+        total = moves = 0
+        while state:
+            # serve whichever lane's count has landed (polling: waiting on one lane in turn
+            # would leave the other lane's stream empty once it runs ahead)
+            ready = [key for key in state if state[key][3][1].query()]
+            if not ready:
+                time.sleep(2e-5)
+                continue
+            for key in ready:
+                ln, left, live, (rc, ev) = state[key]
+                n, stopped = int(ln.count_host[0]), int(ln.count_host[1])
+                rc.n = n
+                if n > 0:
+                    ln.rounds += 1
+                if n > 0 or stopped > 0:
+                    state[key][3] = self._enqueue_round(ln)
+                    continue
+                with self._ctx(ln):
+                    ln.finished = ln.engine.move_end()
+                total += live * self.evaluate_count
+                moves += 1
+                if progress:
+                    progress(self.finished, None)
+                left = None if left is None else left - 1
+                live = begin_move(ln) if left != 0 else 0
+                if live == 0:
+                    del state[key]
+                else:
+                    state[key] = [ln, left, live, self._enqueue_round(ln)]
+        self.moves += moves / len(self.lanes)
+        self.sims += total
+        return total
+
+    def _enqueue_round(self, ln):
+        """Select, network and apply of one round on the lane's stream, no host sync; the
+        round's [pending, stopped] counts are copied to ln.count_host right after the select."""
+        rc = RoundCount()
+        with self._ctx(ln):
+            ln.engine.select_async()
+            ln.engine.count_copy(ln.count_host)
+            ev = torch.cuda.Event()
+            ev.record()
+            p, v = ln.evaluator(None, rc)
+            ln.engine.apply(p, v)
+        return rc, ev
+
     def run(self, game_begin, game_end, seed_base, progress=None):
         self.begin(game_begin, game_end, seed_base)
         t0 = time.time()
-        while self.step():
-            if progress:
-                progress(self.finished, game_end - game_begin)
+        self.steps(None, (lambda f, _: progress(f, game_end - game_begin)) if progress else None)
         return time.time() - t0
 
     def kernel_stats(self, name):
