@@ -404,22 +404,21 @@ def test_fused_selfplay_lanes_are_bit_identical(gpu):
     engines on two streams, network calls overlapping) give the same records bit for
     bit - every kernel computes a board independently of the batch it is in, so cached
     outputs equal fresh ones. The rounds run without a per-round host sync (the count read
-    on the device, SelfPlay._rounds_async) except in the last configuration, the blocking
-    loop: same records and the same number of network rounds."""
+    on the device, lanes pipelined across moves, SelfPlay.steps) except in the last
+    configuration, the blocking lockstep loop: same records. (The number of network rounds may
+    differ by a few: with lanes a move apart, a shared-cache hit can empty a round.)"""
     from uttt_amd.model import calibrated_network
     from uttt_amd.nnfast import FusedNetworkEvaluator
     net = calibrated_network(NETCAL, "cuda")
-    out, rounds = [], []
+    out = []
     for lanes, cache, asy in ((1, 0, True), (1, 16, True), (2, 16, True), (2, 16, False)):
         sp = gpu.SelfPlay(16, 50, 8, 1.0, lanes=lanes, cache_log2=cache)
         sp.async_rounds = asy
         sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng))
         sp.run(0, 12, 4321)
         out.append(sp.records())
-        rounds.append(sp.rounds)
         if cache:
             assert sp.cache_stats()["hits"] > 0
-    assert rounds[2] == rounds[3]
     a = out[0]
     for b in out[1:]:
         assert [r["game"] for r in a] == [r["game"] for r in b] == list(range(12))
