@@ -137,12 +137,15 @@ int uttt_search_select(uttt_engine_t *eng, float *nn_input, int32_t *n_pending);
  * entry points and uttt_search_apply (device results, one row per leaf) read it there, so a
  * round is enqueued with no host synchronisation. A round whose count is 0 changes nothing:
  * the caller enqueues rounds until a count it copied back (uttt_search_count_copy) reads
- * [0] == 0 and [1] == 0, the point where uttt_search_select would report 0. Replaces the
- * per-round blocking read of uttt_search_select for the self-play driver. */
+ * [2] == 0: no tree has simulations left once this round is applied (the next select would
+ * report 0). Replaces the per-round blocking read of uttt_search_select for the self-play
+ * driver. */
 int uttt_search_select_async(uttt_engine_t *eng);
-/* Enqueue a copy of the round's two counts to dst (host, pinned for an asynchronous copy). */
+/* Enqueue a copy of the round's counts to dst[0..2] (host, pinned for an asynchronous copy):
+ * [0] pending leaves, [1] trees stopped by the select budget, [2] trees with simulations left
+ * after this round's apply. */
 int uttt_search_count_copy(uttt_engine_t *eng, int32_t *dst);
-/* Device address of the round's two counts. */
+/* Device address of the round's counts. */
 int uttt_search_count_ptr(uttt_engine_t *eng, const int32_t **count);
 
 /* Host copies of the pending leaves (slot order) and their multiplicity k

@@ -99,7 +99,8 @@ struct Trees {
     int32_t *path;    // [tree][kMaxDepth]
     int32_t *pending; // [tree]
     int32_t *tree_of; // [slot]
-    int32_t *count;   // [0] pending leaves this round, [1] trees stopped by the select budget
+    int32_t *count;   // [0] pending leaves this round, [1] trees stopped by the select budget,
+                      // [2] trees with simulations left after this round's apply
     int32_t n_trees;
     int32_t sims;
     int32_t batch;
@@ -640,7 +641,8 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
                 tr.rec[t] = r;
                 tr.leaf[t] = s;
             }
-            pend = 1;
+            // 3: this leaf's k simulations leave the tree more to do (after its apply)
+            pend = sims_done + k < tr.sims ? 3 : 1;
             break;
         }
         ctl.sims_done = sims_done;
@@ -668,16 +670,19 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);
-    __shared__ int capped;
-    if (tid == 0) capped = 0;
-    int local = 0, cap = 0;
+    __shared__ int capped, more;
+    if (tid == 0) capped = more = 0;
+    int local = 0, cap = 0, mo = 0;
     for (int i = b; i < e; ++i) {
-        local += tr.pending[i] == 1;
-        cap += tr.pending[i] == 2;
+        const int p = tr.pending[i];
+        local += p == 1 || p == 3;
+        cap += p == 2;
+        mo += p >= 2;
     }
     sums[tid] = local;
     __syncthreads();
     if (cap) atomicAdd(&capped, cap);
+    if (mo) atomicAdd(&more, mo);
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
         const int v = tid >= off ? sums[tid - off] : 0;
@@ -687,10 +692,11 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     }
     int slot = sums[tid] - local;
     for (int i = b; i < e; ++i)
-        if (tr.pending[i] == 1) tr.tree_of[slot++] = i;
+        if (tr.pending[i] == 1 || tr.pending[i] == 3) tr.tree_of[slot++] = i;
     if (tid == 1023) {
         tr.count[0] = sums[1023];
         tr.count[1] = capped;
+        tr.count[2] = more;  // trees with simulations left after this round (0: the search ends with it)
     }
 }
 
@@ -1415,7 +1421,7 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     if ((rc = alloc_n(e, &e->tr.ctl, max_trees)) || (rc = alloc_n(e, &e->tr.root, max_trees)) ||
         (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
-        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 2)) ||
+        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)) ||
         (rc = alloc_n(e, &e->d_cache_ctr, 4)))
@@ -1582,7 +1588,7 @@ int uttt_search_select_async(uttt_engine_t *e) {
 int uttt_search_count_copy(uttt_engine_t *e, int32_t *dst) {
     if (!e || !dst) return UTTT_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipMemcpyAsync(dst, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(dst, e->tr.count, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     return UTTT_OK;
 }
 

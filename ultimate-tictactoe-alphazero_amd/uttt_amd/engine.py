@@ -121,11 +121,12 @@ class Engine:
         self.n_pending = None
 
     def count_copy(self, dst):
-        """Enqueue a copy of the round's [pending, stopped] counts into dst (pinned int32 host tensor)."""
+        """Enqueue a copy of the round's [pending, stopped, trees with simulations left after
+        this round] counts into dst (pinned int32 host tensor of >= 3)."""
         check(self.lib.uttt_search_count_copy(self.h, ctypes.c_void_p(dst.data_ptr())))
 
     def count_ptr(self):
-        """Device address of the round's [pending, stopped] counts."""
+        """Device address of the round's counts (see count_copy)."""
         p = ctypes.c_void_p()
         check(self.lib.uttt_search_count_ptr(self.h, ctypes.byref(p)))
         return p

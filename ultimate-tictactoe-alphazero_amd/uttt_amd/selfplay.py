@@ -110,7 +110,7 @@ class _Lane:
         self.evaluator = None
         self.rounds = 0
         self.finished = 0
-        self.count_host = None  # pinned [pending, stopped] of the round in flight (async rounds)
+        self.count_host = None  # pinned counts of the round in flight (async rounds, Engine.count_copy)
 
     def use_stream(self):
         self.engine.use_stream(self.stream)
@@ -246,12 +246,13 @@ class SelfPlay:
         simulations run. With device-count evaluators (FusedNetworkEvaluator) the lanes are
         pipelined. A round's select, network and apply are enqueued without a host sync (the
         pending count stays on the device, Engine.select_async), and the host reads each round's
-        count back - a pinned copy right after the select's scan - only to decide whether to
-        enqueue the next round, while the current round's network still runs; so each lane's
-        stream always holds work. A lane begins its next move as soon as its own move ends, so
-        no lane idles at a move boundary while the other finishes. The sequence of select
-        launches per lane equals the blocking loop's (a round without pending leaves changes
-        nothing), each game depends only on its id, and every lane plays exactly k moves:
+        counts back - a pinned copy right after the select's scan - only to decide whether to
+        enqueue the next round (some tree has simulations left after this one) or end the move,
+        while the current round's network still runs; so each lane's stream always holds work
+        and no round is enqueued that would find nothing. A lane begins its next move as soon as its own move ends, so
+        no lane idles at a move boundary while the other finishes. Per lane the select launches
+        are the blocking loop's minus its final empty one, each game depends only on its id,
+        and every lane plays exactly k moves:
         records and totals are those of k lockstep steps (UTTT_ASYNC_ROUNDS=0)."""
         if not self._device_count():
             total, i = 0, 0
@@ -266,7 +267,7 @@ class SelfPlay:
             return total
         for ln in self.lanes:
             if ln.count_host is None:
-                ln.count_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+                ln.count_host = torch.zeros(3, dtype=torch.int32).pin_memory()
 
         def begin_move(ln):
             with self._ctx(ln):
@@ -287,13 +288,14 @@ class SelfPlay:
                 continue
             for key in ready:
                 ln, left, live, (rc, ev) = state[key]
-                n, stopped = int(ln.count_host[0]), int(ln.count_host[1])
+                n, more = int(ln.count_host[0]), int(ln.count_host[2])
                 rc.n = n
                 if n > 0:
                     ln.rounds += 1
-                if n > 0 or stopped > 0:
+                if more > 0:  # some tree has simulations left once this round is applied
                     state[key][3] = self._enqueue_round(ln)
                     continue
+                # this round (already enqueued) completes the move: move_end follows it on the stream
                 with self._ctx(ln):
                     ln.finished = ln.engine.move_end()
                 total += live * self.evaluate_count
@@ -312,7 +314,7 @@ class SelfPlay:
 
     def _enqueue_round(self, ln):
         """Select, network and apply of one round on the lane's stream, no host sync; the
-        round's [pending, stopped] counts are copied to ln.count_host right after the select."""
+        round's counts are copied to ln.count_host right after the select."""
         rc = RoundCount()
         with self._ctx(ln):
             ln.engine.select_async()
