@@ -194,6 +194,18 @@ int uttt_selfplay_move_end(uttt_engine_t *eng, int64_t *n_finished);
  * afterwards (self_play_cpp.play draws from np.random, self_play_cpp.py:86). */
 int uttt_selfplay_get_rng(uttt_engine_t *eng, int32_t slot, uint32_t key[624], int32_t *pos);
 int uttt_selfplay_set_rng(uttt_engine_t *eng, int32_t slot, const uint32_t key[624], int32_t pos);
+/* The move boundary without host synchronisation, for a driver that pipelines moves
+ * (DESIGN.md §7): uttt_selfplay_move_end_async enqueues the move's end (scores, sampled move,
+ * records, new games for free slots) and a copy of the counters to pinned host memory;
+ * uttt_selfplay_move_begin_async enqueues the next move's roots (the live flags stay on the
+ * device). Once the stream has passed that copy (e.g. an event recorded after it completed),
+ * uttt_selfplay_move_result reports failed trees and a full arena, as move_end does, and
+ * returns the games finished so far and the live slots of the next move. Not with periodic
+ * cache clears (uttt_engine_set_cache clear_every > 0). */
+int uttt_selfplay_move_begin_async(uttt_engine_t *eng);
+int uttt_selfplay_move_end_async(uttt_engine_t *eng);
+int uttt_selfplay_move_result(uttt_engine_t *eng, int64_t *n_finished, int32_t *n_live_next);
+
 /* Finished games: n_games entries of (game id, first ply in arena, plies),
  * sorted by game id; then the arena rows [0, n_plies): state, policy target
  * (81 f64), action, value. Any output pointer may be NULL. */

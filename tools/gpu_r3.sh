@@ -44,7 +44,7 @@ for s in $STEPS; do
            for cfg in "${cfgs[@]}"; do
              name=${cfg%%:*}; rest=${cfg#*:}; envs=""; args=""
              for w in $rest; do case $w in UTTT_*=*) envs="$envs $w" ;; *) args="$args $w" ;; esac; done
-             env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps 10 --warmup 4 $args \
+             env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps ${AB_STEPS:-10} --warmup 4 $args \
                > $OUT/ab_$name.log 2>&1 || exit $?
              echo "$name $(tail -1 $OUT/ab_$name.log | cut -c1-260)" >> $OUT/ab.log
            done ;;

@@ -1007,9 +1007,13 @@ __device__ double np_sum(const double *a, int n) {
 // One thread per slot: the per-move tail of self_play_cpp.play (:63-92). The slot's
 // f64 policy-target row of this ply (81 doubles in HBM) is the working buffer: no
 // per-thread arrays, so nothing lives in scratch.
-__global__ void k_move_end(Pool pool, SelfPlay sp) {
+__global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ ctl, unsigned long long *err) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= sp.slots) return;
+    if (err) {  // the asynchronous move end reports a failed tree through this word
+        const uint32_t st = ctl[s].status;
+        if (st & kErrMask) atomicMin(err, ((unsigned long long)s << 32) | st);
+    }
     Slot sl = sp.slot[s];
     sl.finished = 0;
     if (!sl.live) {
@@ -1174,6 +1178,8 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
         sp.ctr[1] = games0 + fcount[1023];
         const int64_t nxt = next0 + free_sum[1023];
         sp.ctr[0] = nxt < sp.game_end ? nxt : sp.game_end;
+        // live slots for the next move: those still playing plus the free ones given a game
+        sp.ctr[3] = (int64_t)(sp.slots - free_sum[1023]) + (sp.ctr[0] - next0);
     }
 }
 
@@ -1241,6 +1247,8 @@ struct uttt_engine {
     // self-play
     SelfPlay sp{};
     int64_t sp_arena_used = 0;
+    int64_t *h_move = nullptr;          // pinned: [0..3] sp.ctr after the last move end, [4] error word
+    unsigned long long *d_err = nullptr;  // first failed tree of a move: (tree << 32) | status, or ~0
     // evaluation cache (off unless uttt_engine_set_cache)
     EvalCache cache{};
     int cache_log2 = 0;
@@ -1312,15 +1320,21 @@ struct TimedLaunch {
     }
 };
 
-// Called after a stream sync: fold finished event pairs into the totals.
+// Fold finished event pairs into the totals (pairs whose end has not been reached yet, e.g.
+// behind the asynchronous rounds, stay pending).
 void drain_events(uttt_engine *e) {
+    size_t keep = 0;
     for (auto &ev : e->pending_ev) {
+        if (hipEventQuery(ev.b) == hipErrorNotReady) {
+            e->pending_ev[keep++] = ev;
+            continue;
+        }
         float ms = 0.0f;
         if (hipEventElapsedTime(&ms, ev.a, ev.b) == hipSuccess) e->ms[ev.kid] += ms;
         e->ev_pool.push_back(ev.a);
         e->ev_pool.push_back(ev.b);
     }
-    e->pending_ev.clear();
+    e->pending_ev.resize(keep);
 }
 
 unsigned long long *bytes_ptr(uttt_engine *e, int kid) { return e->timing ? e->d_bytes + kid : nullptr; }
@@ -1426,6 +1440,11 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)) ||
         (rc = alloc_n(e, &e->d_cache_ctr, 4)))
         return fail(rc);
+    if ((rc = alloc_n(e, &e->d_err, 1))) return fail(rc);
+    if (hipHostMalloc((void **)&e->h_move, sizeof(int64_t) * 5, hipHostMallocDefault) != hipSuccess) {
+        set_error("hipHostMalloc failed");
+        return fail(UTTT_ERR_HIP);
+    }
     if (hipHostMalloc((void **)&e->h_count, sizeof(int32_t) * 4, hipHostMallocDefault) != hipSuccess) {
         set_error("hipHostMalloc failed");
         return fail(UTTT_ERR_HIP);
@@ -1458,6 +1477,7 @@ int uttt_engine_destroy(uttt_engine_t *e) {
         if (e->cache.val) (void)hipFree(e->cache.val);
     }
     if (e->h_count) (void)hipHostFree(e->h_count);
+    if (e->h_move) (void)hipHostFree(e->h_move);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
     return UTTT_OK;
@@ -1798,7 +1818,9 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp);
     if ((rc = check_launch())) return rc;
+    HIP_TRY(hipMemcpyAsync(e->h_move, sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    e->h_move[4] = -1;
     e->selfplay = true;
     e->sp_arena_used = 0;
     e->moves = 0;
@@ -1852,7 +1874,8 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
     const int slots = e->sp.slots;
     {
         TimedLaunch tl(e, kKMoveEnd);
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 255) / 256), dim3(256), 0, e->stream, e->pool, e->sp);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 255) / 256), dim3(256), 0, e->stream, e->pool, e->sp,
+                           (const TreeCtl *)nullptr, (unsigned long long *)nullptr);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
     }
@@ -1868,6 +1891,84 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
     e->sp_arena_used = ctr[2];
     if (n_finished) *n_finished = ctr[1];
     e->phase = 0;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_move_begin_async(uttt_engine_t *e) {
+    if (!e || !e->selfplay) {
+        set_error("uttt_selfplay_move_begin_async: call uttt_selfplay_begin first");
+        return UTTT_ERR_ORDER;
+    }
+    if (e->phase != 0) {
+        set_error("uttt_selfplay_move_begin_async: the previous move was not ended");
+        return UTTT_ERR_ORDER;
+    }
+    if (e->cache.flag && e->cache_clear_every > 0) {
+        set_error("uttt_selfplay_move_begin_async: periodic cache clears need the blocking move_begin");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    const int slots = e->sp.slots;
+    e->tr.n_trees = slots;
+    e->moves++;
+    HIP_TRY(hipMemcpy2DAsync(e->tr.leaf, sizeof(uttt_state_t), e->sp.slot, sizeof(Slot), sizeof(uttt_state_t), slots,
+                             hipMemcpyDeviceToDevice, e->stream));
+    hipLaunchKernelGGL(k_begin, dim3(grid_waves(slots)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+                       (const uttt_state_t *)e->tr.leaf, (const int32_t *)e->sp.live);
+    int rc = check_launch();
+    if (rc) return rc;
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_move_end_async(uttt_engine_t *e) {
+    if (!e || !e->selfplay) {
+        set_error("uttt_selfplay_move_end_async: call uttt_selfplay_begin first");
+        return UTTT_ERR_ORDER;
+    }
+    if (e->phase != 1) {
+        set_error("uttt_selfplay_move_end_async: no move in progress, or pending leaves were not applied");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    const int slots = e->sp.slots;
+    HIP_TRY(hipMemsetAsync(e->d_err, 0xFF, sizeof(unsigned long long), e->stream));
+    {
+        TimedLaunch tl(e, kKMoveEnd);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 255) / 256), dim3(256), 0, e->stream, e->pool, e->sp,
+                           (const TreeCtl *)e->tr.ctl, e->d_err);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
+        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
+    }
+    int rc = check_launch();
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(e->h_move, e->sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->h_move + 4, e->d_err, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream));
+    e->phase = 0;
+    return UTTT_OK;
+}
+
+int uttt_selfplay_move_result(uttt_engine_t *e, int64_t *n_finished, int32_t *n_live_next) {
+    if (!e || !e->selfplay) return UTTT_ERR_ORDER;
+    const unsigned long long err = (unsigned long long)e->h_move[4];
+    if (err != ~0ull) {
+        const uint32_t st = (uint32_t)err, t = (uint32_t)(err >> 32);
+        set_error("tree %u failed (status 0x%x: %s)", t, st,
+                  (st & kErrCapacity) ? "node pool exhausted"
+                  : (st & kErrDepth)  ? "path deeper than 128"
+                                      : "no selectable child (NaN statistics)");
+        return (st & kErrSelect) ? UTTT_ERR_ARG : UTTT_ERR_CAPACITY;
+    }
+    if (e->h_move[2] > e->sp.arena_cap) {
+        set_error("self-play record arena full (%lld plies > %lld)", (long long)e->h_move[2],
+                  (long long)e->sp.arena_cap);
+        return UTTT_ERR_CAPACITY;
+    }
+    e->sp_arena_used = e->h_move[2];
+    drain_events(e);
+    if (n_finished) *n_finished = e->h_move[1];
+    if (n_live_next) *n_live_next = (int32_t)e->h_move[3];
     return UTTT_OK;
 }
 

@@ -192,6 +192,21 @@ class Engine:
         check(self.lib.uttt_selfplay_move_end(self.h, ctypes.byref(n)))
         return n.value
 
+    def move_begin_async(self):
+        """Enqueue the next move's roots without reading the live count (move_result gives it)."""
+        check(self.lib.uttt_selfplay_move_begin_async(self.h))
+
+    def move_end_async(self):
+        """Enqueue the move's end and a copy of its counters; read them with move_result once the
+        stream has passed it."""
+        check(self.lib.uttt_selfplay_move_end_async(self.h))
+
+    def move_result(self):
+        """(games finished so far, live slots of the next move) of the last move_end_async."""
+        f, n = ctypes.c_int64(), ctypes.c_int32()
+        check(self.lib.uttt_selfplay_move_result(self.h, ctypes.byref(f), ctypes.byref(n)))
+        return f.value, n.value
+
     def get_rng(self, slot=0):
         key = np.zeros(624, np.uint32)
         pos = ctypes.c_int32()

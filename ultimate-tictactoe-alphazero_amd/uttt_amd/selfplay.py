@@ -111,6 +111,16 @@ class _Lane:
         self.rounds = 0
         self.finished = 0
         self.count_host = None  # pinned counts of the round in flight (async rounds, Engine.count_copy)
+        self.spec = True        # enqueue the next round's network before its count is known
+        self._no_rows = None
+
+    def no_rows(self):
+        """(policy, value) device buffers for an apply with no pending leaf (nothing is read)."""
+        if self._no_rows is None:
+            dev = torch.device("cuda", self.engine.device)
+            self._no_rows = (torch.zeros((1, 81), dtype=torch.float32, device=dev),
+                             torch.zeros((1,), dtype=torch.float32, device=dev))
+        return self._no_rows
 
     def use_stream(self):
         self.engine.use_stream(self.stream)
@@ -156,6 +166,7 @@ class SelfPlay:
             self.evaluator = evaluator
         self.sims = 0
         self.moves = 0
+        self.cache_clear_every = cache_clear_every  # periodic clears need the blocking move boundary
         # rounds without a per-round host sync when every lane's evaluator reads the count on
         # the device (FusedNetworkEvaluator); UTTT_ASYNC_ROUNDS=0 keeps the blocking loop
         self.async_rounds = os.environ.get("UTTT_ASYNC_ROUNDS", "1") != "0"
@@ -207,7 +218,8 @@ class SelfPlay:
         self.sims = self.moves = 0
 
     def _device_count(self):
-        return self.async_rounds and all(getattr(ln.evaluator, "device_count", False) for ln in self.lanes)
+        return (self.async_rounds and not self.cache_clear_every and
+                all(getattr(ln.evaluator, "device_count", False) for ln in self.lanes))
 
     def step(self):
         """One move for every live game. Returns the simulations it ran (0 = all games over)."""
@@ -249,8 +261,10 @@ class SelfPlay:
         counts back - a pinned copy right after the select's scan - only to decide whether to
         enqueue the next round (some tree has simulations left after this one) or end the move,
         while the current round's network still runs; so each lane's stream always holds work
-        and no round is enqueued that would find nothing. A lane begins its next move as soon as its own move ends, so
-        no lane idles at a move boundary while the other finishes. Per lane the select launches
+        and no round is enqueued that would find nothing. A lane's move end and its next move's
+        roots are enqueued the same way (Engine.move_end_async / move_begin_async; the counters
+        are read when they have landed), so no lane idles at a move boundary, neither for the
+        host nor for the other lane. Per lane the select launches
         are the blocking loop's minus its final empty one, each game depends only on its id,
         and every lane plays exactly k moves:
         records and totals are those of k lockstep steps (UTTT_ASYNC_ROUNDS=0)."""
@@ -269,61 +283,91 @@ class SelfPlay:
             if ln.count_host is None:
                 ln.count_host = torch.zeros(3, dtype=torch.int32).pin_memory()
 
-        def begin_move(ln):
-            with self._ctx(ln):
-                return ln.engine.move_begin()
-
         state = {}
         for ln in self.lanes:
-            live = begin_move(ln)
+            with self._ctx(ln):
+                live = ln.engine.move_begin()  # the first move of the call: blocking, gives the live count
             if live > 0:
-                state[id(ln)] = [ln, k, live, self._enqueue_round(ln)]
+                ln.cur_live = live
+                ln.moves_left = k
+                ln.result_pending = False
+                state[id(ln)] = (ln, self._enqueue_round(ln, ln.spec))
         total = moves = 0
         while state:
             # serve whichever lane's count has landed (polling: waiting on one lane in turn
             # would leave the other lane's stream empty once it runs ahead)
-            ready = [key for key in state if state[key][3][1].query()]
+            ready = [key for key in state if state[key][1][1].query()]
             if not ready:
                 time.sleep(2e-5)
                 continue
             for key in ready:
-                ln, left, live, (rc, ev) = state[key]
+                ln, (rc, ev, spec) = state[key]
+                if ln.result_pending:  # the previous move's end: its counters landed before this count
+                    ln.finished, ln.cur_live = ln.engine.move_result()
+                    ln.result_pending = False
+                    if progress:
+                        progress(self.finished, None)
                 n, more = int(ln.count_host[0]), int(ln.count_host[2])
                 rc.n = n
                 if n > 0:
                     ln.rounds += 1
-                if more > 0:  # some tree has simulations left once this round is applied
-                    state[key][3] = self._enqueue_round(ln)
+                if not spec:  # the network was held back until the count was known
+                    with self._ctx(ln):
+                        if n > 0:
+                            p, v = ln.evaluator(None, rc)
+                            ln.engine.apply(p, v)
+                        else:
+                            ln.engine.apply(*ln.no_rows())
+                ln.spec = n > 0  # a round with leaves predicts another
+                if ln.cur_live == 0:  # every game of the lane is over: this move was empty
+                    del state[key]
                     continue
-                # this round (already enqueued) completes the move: move_end follows it on the stream
-                with self._ctx(ln):
-                    ln.finished = ln.engine.move_end()
-                total += live * self.evaluate_count
+                if more > 0:  # some tree has simulations left once this round is applied
+                    state[key] = (ln, self._enqueue_round(ln, ln.spec))
+                    continue
+                # this round (already enqueued) completes the move: end it and begin the next,
+                # both on the stream, without waiting
+                total += ln.cur_live * self.evaluate_count
                 moves += 1
+                ln.moves_left = None if ln.moves_left is None else ln.moves_left - 1
+                with self._ctx(ln):
+                    ln.engine.move_end_async()
+                    ln.result_pending = True
+                    if ln.moves_left == 0:
+                        ev_end = torch.cuda.Event()
+                        ev_end.record()
+                        ln.end_event = ev_end
+                        del state[key]
+                        continue
+                    ln.engine.move_begin_async()
+                state[key] = (ln, self._enqueue_round(ln, ln.spec))
+        for ln in self.lanes:  # the last move's counters
+            if getattr(ln, "result_pending", False):
+                ln.end_event.synchronize()
+                ln.finished, ln.cur_live = ln.engine.move_result()
+                ln.result_pending = False
                 if progress:
                     progress(self.finished, None)
-                left = None if left is None else left - 1
-                live = begin_move(ln) if left != 0 else 0
-                if live == 0:
-                    del state[key]
-                else:
-                    state[key] = [ln, left, live, self._enqueue_round(ln)]
         self.moves += moves / len(self.lanes)
         self.sims += total
         return total
 
-    def _enqueue_round(self, ln):
-        """Select, network and apply of one round on the lane's stream, no host sync; the
-        round's counts are copied to ln.count_host right after the select."""
+    def _enqueue_round(self, ln, spec):
+        """Select of one round on the lane's stream, its counts copied to ln.count_host right
+        after it, and - speculatively, when the lane's previous round had leaves - the network
+        and apply, all without a host sync. Otherwise (a lane whose rounds are answered by the
+        cache or by terminal positions: the network would run empty) the host enqueues the
+        network once the count shows leaves."""
         rc = RoundCount()
         with self._ctx(ln):
             ln.engine.select_async()
             ln.engine.count_copy(ln.count_host)
             ev = torch.cuda.Event()
             ev.record()
-            p, v = ln.evaluator(None, rc)
-            ln.engine.apply(p, v)
-        return rc, ev
+            if spec:
+                p, v = ln.evaluator(None, rc)
+                ln.engine.apply(p, v)
+        return rc, ev, spec
 
     def run(self, game_begin, game_end, seed_base, progress=None):
         self.begin(game_begin, game_end, seed_base)
