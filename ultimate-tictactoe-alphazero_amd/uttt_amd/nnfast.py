@@ -171,40 +171,66 @@ class FusedNetworkEvaluator:
                                            self._stream()))
         return self._tower_heads(n, softmax)
 
+    def _dev_plan(self, stream, n_dev):
+        """The device-count forward's 32 conv argument tuples (fixed buffers and weights), built
+        once per (stream, count): the per-round host cost is then one ctypes call per kernel."""
+        key = (stream.value, n_dev.value)
+        if getattr(self, "_plan", None) is None or self._plan[0] != key:
+            rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
+            cap = self.max_batch
+            x, t, y = (ctypes.c_void_p(b.data_ptr()) for b in self.buf)
+            calls, i = [], 0
+            for (u1, s1, b1), (u2, s2, b2) in self.wino:
+                src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
+                calls.append((x, _p(u1), ctypes.c_float(s1), _p(b1), None, t, src[0], src[1], rows[i % 4],
+                              rows[(i + 1) % 4], cap, n_dev, cap, stream))
+                i += 1
+                calls.append((t, _p(u2), ctypes.c_float(s2), _p(b2), x, y, rows[(i - 1) % 4], 1, rows[i % 4],
+                              rows[(i + 1) % 4], cap, n_dev, cap, stream))
+                i += 1
+                x, y = y, x
+            heads = (x, _p(self.heads), n_dev, cap, _p(self.policy), _p(self.value))
+            self._plan = (key, calls, heads)
+        return self._plan
+
     def _tower_heads(self, n, softmax, n_dev=None):
         stream = self._stream()
+        if n_dev is not None:
+            _, calls, heads = self._dev_plan(stream, n_dev)
+            if self.tower_events is not None:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            fn = self.lib.uttt_nn_conv3x3_wino3h_dev
+            for a in calls:
+                check(fn(*a))
+            if self.tower_events is not None:
+                ev1.record()
+                self.tower_events.append((n, ev0, ev1))
+            check(self.lib.uttt_nn_heads_dev(*heads, 1 if softmax else 0, stream))
+            return self.policy, self.value
         x, t, y = self.buf
         if self.tower_events is not None:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
         rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
         cap = self.max_batch
-        if n_dev is None:
-            fn = self.lib.uttt_nn_conv3x3_wino3h
-            count = (n,)
-        else:  # the count on the device, grids sized for max_batch
-            fn = self.lib.uttt_nn_conv3x3_wino3h_dev
-            count = (n_dev, cap)
+        fn = self.lib.uttt_nn_conv3x3_wino3h
         i = 0
         for (u1, s1, b1), (u2, s2, b2) in self.wino:
             src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
             check(fn(_p(x), _p(u1), ctypes.c_float(s1), _p(b1), None, _p(t), src[0], src[1], rows[i % 4],
-                     rows[(i + 1) % 4], cap, *count, stream))
+                     rows[(i + 1) % 4], cap, n, stream))
             i += 1
             check(fn(_p(t), _p(u2), ctypes.c_float(s2), _p(b2), _p(x), _p(y), rows[(i - 1) % 4], 1, rows[i % 4],
-                     rows[(i + 1) % 4], cap, *count, stream))
+                     rows[(i + 1) % 4], cap, n, stream))
             i += 1
             x, y = y, x
         if self.tower_events is not None:
             ev1.record()
             self.tower_events.append((n, ev0, ev1))
-        if n_dev is None:
-            check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
-                                         1 if softmax else 0, stream))
-            return self.policy[:n], self.value[:n]
-        check(self.lib.uttt_nn_heads_dev(_p(x), _p(self.heads), n_dev, cap, _p(self.policy), _p(self.value),
-                                         1 if softmax else 0, stream))
-        return self.policy, self.value
+        check(self.lib.uttt_nn_heads(_p(x), _p(self.heads), n, _p(self.policy), _p(self.value),
+                                     1 if softmax else 0, stream))
+        return self.policy[:n], self.value[:n]
 
     def __call__(self, x, n):
         return self.forward(n, True)
