@@ -682,7 +682,9 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     sums[tid] = local;
     __syncthreads();
     if (cap) atomicAdd(&capped, cap);
-    if (mo) atomicAdd(&more, mo);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mo += __shfl_xor(mo, off);  // one LDS atomic per wave
+    if ((tid & 63) == 0 && mo) atomicAdd(&more, mo);
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
         const int v = tid >= off ? sums[tid - off] : 0;
