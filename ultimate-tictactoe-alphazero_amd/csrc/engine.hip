@@ -1043,7 +1043,9 @@ __global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ c
         const double y = (double)(1.0f / sp.temperature);  // glibc powf: double pow, one rounding
         float sum = 0.0f;
         for (int i = 0; i < L; ++i) {
-            const float v = (float)pow((double)pool.n[base + first + i], y);
+            // pow(x, 1) == x exactly (IEEE 754): the self-play temperature 1.0 skips the call
+            const double xn = (double)pool.n[base + first + i];
+            const float v = (float)(y == 1.0 ? xn : pow(xn, y));
             pt[i] = (double)v;
             sum += v;
         }
@@ -1876,7 +1878,7 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
     const int slots = e->sp.slots;
     {
         TimedLaunch tl(e, kKMoveEnd);
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 255) / 256), dim3(256), 0, e->stream, e->pool, e->sp,
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp,
                            (const TreeCtl *)nullptr, (unsigned long long *)nullptr);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
@@ -1938,7 +1940,7 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
     HIP_TRY(hipMemsetAsync(e->d_err, 0xFF, sizeof(unsigned long long), e->stream));
     {
         TimedLaunch tl(e, kKMoveEnd);
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 255) / 256), dim3(256), 0, e->stream, e->pool, e->sp,
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp,
                            (const TreeCtl *)e->tr.ctl, e->d_err);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
