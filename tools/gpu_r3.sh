@@ -36,6 +36,7 @@ for s in $STEPS; do
     vsmall) VARIANTS= timeout -k 10 300 python -u tools/diag/wino3h_variants.py 250 500 1000 > $OUT/variants_small.log 2>&1 ;;
     tcomp) timeout -k 10 600 python -u tools/diag/train_compare.py > $OUT/train_compare.log 2>&1 ;;
     tcheck) timeout -k 10 300 python -u tools/diag/train_graph_check.py > $OUT/train_check.log 2>&1 ;;
+    heads) timeout -k 10 300 python -u tools/diag/heads_bits.py > $OUT/heads_bits.log 2>&1 ;;
     vars)  timeout -k 10 300 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
     ab)    # A/B of launch shapes on the headline workload (short runs, one JSON line each)
            cfgs=("base:" "grid0:UTTT_WINO3H_GRID=0" "grid2:UTTT_WINO3H_GRID=2" "lanes1:--lanes 1"

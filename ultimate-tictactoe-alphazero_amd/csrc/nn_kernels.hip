@@ -90,21 +90,29 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
 
 // Head weight block (uttt_nn.h UTTT_HEAD_*): folded 1x1 convs, then the FC layers with
 // their weights stored input-major (consecutive threads = consecutive outputs read
-// consecutive floats). HB positions per workgroup share every weight load; the kernel is
-// latency-bound (chains of L2 weight loads), so more, smaller workgroups win: 1,344 boards
-// take 120 / 73 / 60 / 53 / 52 us at HB = 16 / 8 / 4 / 2 / 1 (tools/diag/nn_parts.py).
-constexpr int HB = 1;
-__global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, const float *__restrict__ hw, int n,
-                                               const int32_t *__restrict__ n_dev, float *__restrict__ policy,
-                                               float *__restrict__ value, int softmax) {
+// consecutive floats). The two FC weight matrices (132 KB) are staged in LDS once per
+// workgroup and shared by its HB boards: with HB = 1 every board streamed them from L2 in
+// chains of dependent loads (84 us for 1,380 boards in the bench, round 3). Each board's
+// arithmetic - order of every sum included - is the same for any HB.
+constexpr int HB = 8;
+constexpr int HT = 1024;  // threads: 1x1 convs in 64 groups of 16 lanes, FC1 as 4 board groups x 256 units
+__global__ __launch_bounds__(HT) void k_heads(const float *__restrict__ act, const float *__restrict__ hw, int n,
+                                              const int32_t *__restrict__ n_dev, float *__restrict__ policy,
+                                              float *__restrict__ value, int softmax) {
+    __shared__ float s_pw[162 * 81];   // policy FC W^T [162][81]
+    __shared__ float s_w1[81 * 256];   // value FC1 W^T [81][256]
     __shared__ float s_h[HB][3 * 81];  // relu(1x1 conv): [p0 | p1 | v] x 81 (NCHW flatten order)
     __shared__ float s_z[HB][81];      // policy logits
-    __shared__ float s_v[HB][4];       // value FC2 partial sums, one per wave
+    __shared__ float s_v[HB][4];       // value FC2 partial sums, one per 64 units
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int b0 = blockIdx.x * HB;
     if (n_dev) n = min(n, *n_dev);
     if (b0 >= n) return;
     const int nb = n - b0 < HB ? n - b0 : HB;
+#pragma unroll 4
+    for (int i = t; i < 162 * 81; i += HT) s_pw[i] = hw[UTTT_HEAD_PFC_W + i];
+#pragma unroll 4
+    for (int i = t; i < 81 * 256; i += HT) s_w1[i] = hw[UTTT_HEAD_VFC1_W + i];
     // 1x1 convs (128 -> 2 policy planes, 128 -> 1 value plane) + ReLU: 16 lanes per
     // (position, board), 8 channels per lane, 16-lane shuffle reduction
     {
@@ -117,8 +125,7 @@ __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, co
             w2[k] = hw[UTTT_HEAD_VCONV_W + 8 * g + k];
         }
         const float c0 = hw[UTTT_HEAD_PCONV_B], c1 = hw[UTTT_HEAD_PCONV_B + 1], c2 = hw[UTTT_HEAD_VCONV_B];
-#pragma unroll 4
-        for (int i = t >> 4; i < nb * 81; i += 16) {
+        for (int i = t >> 4; i < nb * 81; i += HT / 16) {
             const float4 *src = reinterpret_cast<const float4 *>(act + ((size_t)b0 * 81 + i) * C + 8 * g);
             const float4 xa = src[0], xb = src[1];
             const float x[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
@@ -144,53 +151,42 @@ __global__ __launch_bounds__(256) void k_heads(const float *__restrict__ act, co
         }
     }
     __syncthreads();
-    // value FC1 (81 -> 256) + ReLU, thread t = unit t; FC2 (256 -> 1) partial sums per wave
+    // value FC1 (81 -> 256) + ReLU: unit u = t % 256 of boards q, q + 4 (q = t / 256); FC2
+    // (256 -> 1) partial sums per 64 units, combined in the same order for every board
     {
-        float acc[HB];
-        const float bt = hw[UTTT_HEAD_VFC1_B + t];
+        const int u = t & 255, q = t >> 8;
+        constexpr int BQ = HB / 4;
+        float acc[BQ];
+        const float bt = hw[UTTT_HEAD_VFC1_B + u];
 #pragma unroll
-        for (int bi = 0; bi < HB; ++bi) acc[bi] = bt;
-        const float *w1 = hw + UTTT_HEAD_VFC1_W + t;  // W1^T [81][256]
-        // unrolled: 9 weight loads in flight instead of one L2 round trip per input (the
-        // accumulation order per board is unchanged)
+        for (int r = 0; r < BQ; ++r) acc[r] = bt;
 #pragma unroll 9
         for (int j = 0; j < 81; ++j) {
-            const float wj = w1[j * 256];
+            const float wj = s_w1[j * 256 + u];
 #pragma unroll
-            for (int bi = 0; bi < HB; ++bi) acc[bi] += wj * s_h[bi][162 + j];
+            for (int r = 0; r < BQ; ++r) acc[r] += wj * s_h[q + 4 * r][162 + j];
         }
-        const float w2 = hw[UTTT_HEAD_VFC2_W + t];
+        const float w2 = hw[UTTT_HEAD_VFC2_W + u];
 #pragma unroll
-        for (int bi = 0; bi < HB; ++bi) {
-            float v = w2 * fmaxf(acc[bi], 0.0f);
+        for (int r = 0; r < BQ; ++r) {
+            float v = w2 * fmaxf(acc[r], 0.0f);
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if (lane == 0) s_v[bi][wv] = v;
+            if (lane == 0) s_v[q + 4 * r][u >> 6] = v;
         }
     }
-    // policy FC (162 -> 81): thread t < 81 * 3 = output t % 81 for boards t / 81, + 3, ...
-    if (t < 243) {
-        const int o = t % 81, g = t / 81;
-        float z[(HB + 2) / 3];
-        const float bo = hw[UTTT_HEAD_PFC_B + o];
-#pragma unroll
-        for (int r = 0; r < (HB + 2) / 3; ++r) z[r] = bo;
-        const float *wp = hw + UTTT_HEAD_PFC_W + o;  // Wp^T [162][81]
+    // policy FC (162 -> 81): thread t < 81 * HB = output t % 81 of board t / 81
+    if (t < 81 * HB) {
+        const int o = t % 81, bi = t / 81;
+        float z = hw[UTTT_HEAD_PFC_B + o];
 #pragma unroll 9
-        for (int j = 0; j < 162; ++j) {
-            const float wj = wp[j * 81];
-#pragma unroll
-            for (int r = 0; r < (HB + 2) / 3; ++r)
-                if (g + 3 * r < HB) z[r] += wj * s_h[g + 3 * r][j];
-        }
-#pragma unroll
-        for (int r = 0; r < (HB + 2) / 3; ++r)
-            if (g + 3 * r < HB) s_z[g + 3 * r][o] = z[r];
+        for (int j = 0; j < 162; ++j) z += s_pw[j * 81 + o] * s_h[bi][j];
+        s_z[bi][o] = z;
     }
     __syncthreads();
     if (t < nb) value[b0 + t] = tanhf(((s_v[t][0] + s_v[t][1]) + (s_v[t][2] + s_v[t][3])) + hw[UTTT_HEAD_VFC2_B]);
     // softmax over the 81 logits of a board: one wave per board, lanes hold z[lane], z[lane + 64]
-    for (int bi = wv; bi < nb; bi += 4) {
+    for (int bi = wv; bi < nb; bi += HT / 64) {
         float *po = policy + (size_t)(b0 + bi) * 81;
         const bool two = lane + 64 < 81;
         const float z0 = s_z[bi][lane], z1 = two ? s_z[bi][lane + 64] : -INFINITY;
@@ -265,7 +261,7 @@ int uttt_nn_heads(const float *act, const float *head_weights, int32_t n, float 
         return UTTT_ERR_ARG;
     }
     if (n == 0) return UTTT_OK;
-    hipLaunchKernelGGL(nn::k_heads, dim3((n + nn::HB - 1) / nn::HB), dim3(256), 0, (hipStream_t)stream, act, head_weights, n,
+    hipLaunchKernelGGL(nn::k_heads, dim3((n + nn::HB - 1) / nn::HB), dim3(nn::HT), 0, (hipStream_t)stream, act, head_weights, n,
                        (const int32_t *)nullptr, policy, value, softmax ? 1 : 0);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
@@ -282,7 +278,7 @@ int uttt_nn_heads_dev(const float *act, const float *head_weights, const int32_t
         return UTTT_ERR_ARG;
     }
     if (max_n == 0) return UTTT_OK;
-    hipLaunchKernelGGL(nn::k_heads, dim3((max_n + nn::HB - 1) / nn::HB), dim3(256), 0, (hipStream_t)stream, act,
+    hipLaunchKernelGGL(nn::k_heads, dim3((max_n + nn::HB - 1) / nn::HB), dim3(nn::HT), 0, (hipStream_t)stream, act,
                        head_weights, max_n, n_dev, policy, value, softmax ? 1 : 0);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
