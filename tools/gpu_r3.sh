@@ -49,6 +49,18 @@ for s in $STEPS; do
                > $OUT/ab_$name.log 2>&1 || exit $?
              echo "$name $(tail -1 $OUT/ab_$name.log | cut -c1-260)" >> $OUT/ab.log
            done ;;
+    abl)   # same-box A/B of the engine library: the in-tree build against libuttt_engine_base.so (a build of
+           # the previous engine.hip), alternating base / new, headline workload and tree-only
+           for i in 1 2; do
+             for lib in base new; do
+               envs=""; [ $lib = base ] && envs="UTTT_ENGINE_LIB=$PWD/ultimate-tictactoe-alphazero_amd/libuttt_engine_base.so"
+               for ev in fused hash; do
+                 env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps ${AB_STEPS:-10} --warmup 4 \
+                   --evaluator $ev > $OUT/abl_${lib}_${ev}_$i.log 2>&1 || exit $?
+                 echo "$lib $ev $i $(tail -1 $OUT/abl_${lib}_${ev}_$i.log | cut -c1-200)" >> $OUT/abl.log
+               done
+             done
+           done ;;
     bench) timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 ;;
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/prof_bench.log 2>&1 ;;

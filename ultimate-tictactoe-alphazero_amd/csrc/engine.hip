@@ -152,6 +152,29 @@ __device__ __forceinline__ void wave_argmax(float &v, int &i) {
     }
 }
 
+// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction):
+// within each row of 16 lanes (quad swaps, half-row and row mirrors), then row 0 into row 1
+// and row 2 into row 3 (row_bcast15), then row 1 into rows 2-3 (row_bcast31). The order
+// (larger value, then smaller index) is total, so any reduction tree gives the same winner;
+// the result is valid in lane 63.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void argmax_dpp(float &v, int &i) {
+    const int vb = __float_as_int(v);
+    const float ov = __int_as_float(__builtin_amdgcn_update_dpp(vb, vb, CTRL, ROWS, 0xF, false));
+    const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, ROWS, 0xF, false);
+    const bool take = ov > v || (ov == v && oi < i);
+    v = take ? ov : v;
+    i = take ? oi : i;
+}
+__device__ __forceinline__ void wave_argmax_to63(float &v, int &i) {
+    argmax_dpp<0xB1, 0xF>(v, i);   // quad_perm [1,0,3,2]
+    argmax_dpp<0x4E, 0xF>(v, i);   // quad_perm [2,3,0,1]
+    argmax_dpp<0x141, 0xF>(v, i);  // row_half_mirror
+    argmax_dpp<0x140, 0xF>(v, i);  // row_mirror
+    argmax_dpp<0x142, 0xA>(v, i);  // row_bcast15 -> rows 1, 3
+    argmax_dpp<0x143, 0xC>(v, i);  // row_bcast31 -> rows 2, 3
+}
+
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -225,9 +248,9 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
     const uint32_t slot = (h + (uint32_t)lane) & c.mask;
     uint32_t f = 0u;
     bool same = false;
-    if (lane < kProbe) {
+    if (lane < kProbe) {  // flag and key in one round trip (the key only counts when the flag is 2)
         f = ld_agent(c.flag + slot);
-        if (f == 2u) same = key_is(c, slot, s);
+        same = key_is(c, slot, s);
     }
     const uint64_t hit = __ballot(lane < kProbe && f == 2u && same);
     const uint64_t empty = __ballot(lane < kProbe && f == 0u);
@@ -262,10 +285,30 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
     if (!c.flag) return;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
+    // the kProbe slots' flags and keys in one round trip (lanes 0..kProbe-1), then lane 0 acts on
+    // the first slot that holds this position or is empty; a lost claim falls back to probing
+    // one slot after another from there
+    const uint32_t h = state_hash(s);
+    uint32_t f = 0u;
+    bool same = false;
+    if (lane < kProbe) {
+        const uint32_t sl = (h + (uint32_t)lane) & c.mask;
+        f = ld_agent(c.flag + sl);
+        same = key_is(c, sl, s);
+    }
+    const uint64_t here = __ballot(lane < kProbe && f == 2u && same);
+    const uint64_t free_ = __ballot(lane < kProbe && f == 0u);
+    const uint64_t either = here | free_;
+    const int first = either ? __builtin_ctzll(either) : kProbe;
     if (lane == 0) {
-        const uint32_t h = state_hash(s);
-        bool present = false;
-        for (int i = 0; i < kProbe; ++i) {
+        bool present = first < kProbe && ((here >> first) & 1ull);
+        int i0 = first;
+        if (!present && first < kProbe) {
+            const uint32_t sl = (h + (uint32_t)first) & c.mask;
+            if (atomicCAS(c.flag + sl, 0u, 1u) == 0u) slot = (int)sl;
+            else i0 = first + 1;
+        }
+        for (int i = i0; slot < 0 && !present && i < kProbe; ++i) {
             const uint32_t sl = (h + (uint32_t)i) & c.mask;
             const uint32_t f = ld_agent(c.flag + sl);
             if (f == 2u && key_is(c, sl, s)) {
@@ -480,8 +523,10 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 // (pending = 2) and resumes in the next launch from the same point: the sequence of
 // simulations per tree, hence every result, is unchanged; only the tail of the launch is cut.
 constexpr int kSelectBudget = 8;
+constexpr int kScanGroup = 4;  // child-scan iterations (64 children each) whose loads are issued together
 
-__global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCache cache,
+template <bool PY>
+__global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalCache cache,
                                                    unsigned long long *stats) {
     __shared__ float s_hit[kWavesPerBlock][kCacheVal];  // a cache hit's values, per wave
     const int lane = lane_id();
@@ -504,32 +549,67 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
             int node = 0, depth = 0;
             int path_lo = 0, path_hi = 0;  // lane d: path[d], path[64 + d]
             uint2 lk = LK[0];
+            int node_n = N[0];  // the current node's visits (below the root: from the parent's scan)
             bool fail = false;
             for (;;) {
-                const int cnt = tr.py ? meta_L(lk.y) : meta_k(lk.y) * meta_L(lk.y);
+                const int cnt = PY ? meta_L(lk.y) : meta_k(lk.y) * meta_L(lk.y);
                 if (cnt == 0) break;
                 const int first = (int)lk.x;
-                const int kself = (node == 0 && !tr.py) ? 0 : meta_k(lk.y);
-                const int total = N[node] - kself;  // == sum of children's visits
+                const int kself = (node == 0 && !PY) ? 0 : meta_k(lk.y);
                 int bi = kNone;
-                if (!tr.py) {
+                if (!PY) {
+                    const int total = node_n - kself;  // == sum of children's visits
                     const float sq = sqrtf((float)total);
                     float best = -1e9f;
-                    for (int c = lane; c < cnt; c += kWave) {
-                        const int cn = N[first + c];
-                        const float cw = W[first + c];
-                        const float cp = P[first + c];
-                        // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off)
-                        const float q = (cn > 0) ? (-cw / (float)cn) : 0.0f;
-                        const float u = cp * sq / (float)(1 + cn);
-                        const float v = q + u;
-                        if (v > best) {
-                            best = v;
-                            bi = c;
+                    int bn = 0;
+                    uint2 bl = make_uint2(0u, 0u);
+                    // Every load of a group of kScanGroup x 64 children is issued before the first
+                    // compare (one memory round trip per group; a node expanded by a flush of k = 8
+                    // copies has up to 8 x 81 children), and each child's link word and visits come
+                    // with it, so the winner's are read from its lane's registers instead of from
+                    // memory after the arg-max: one dependent round trip per level.
+                    for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
+                        int cn[kScanGroup];
+                        float cw[kScanGroup], cp[kScanGroup];
+                        uint2 cl[kScanGroup];
+#pragma unroll
+                        for (int j = 0; j < kScanGroup; ++j) {
+                            if (c0 + j * kWave < cnt) {  // wave-uniform
+                                const int c = min(c0 + j * kWave + lane, cnt - 1);
+                                cn[j] = N[first + c];
+                                cw[j] = W[first + c];
+                                cp[j] = P[first + c];
+                                cl[j] = LK[first + c];
+                            }
+                        }
+#pragma unroll
+                        for (int j = 0; j < kScanGroup; ++j) {
+                            if (c0 + j * kWave < cnt) {
+                                const int c = c0 + j * kWave + lane;
+                                // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off);
+                                // the per-lane scan stays strict '>' in child order
+                                const float q = (cn[j] > 0) ? (-cw[j] / (float)cn[j]) : 0.0f;
+                                const float u = cp[j] * sq / (float)(1 + cn[j]);
+                                const float v = q + u;
+                                const bool take = c < cnt && v > best;
+                                best = take ? v : best;
+                                bi = take ? c : bi;
+                                bn = take ? cn[j] : bn;
+                                bl.x = take ? cl[j].x : bl.x;
+                                bl.y = take ? cl[j].y : bl.y;
+                            }
                         }
                     }
-                    wave_argmax(best, bi);
+                    wave_argmax_to63(best, bi);
+                    bi = __builtin_amdgcn_readlane(bi, 63);
+                    if (bi != kNone) {  // the winner's lane holds its visits and link word
+                        const int wl = bi & (kWave - 1);
+                        node_n = __builtin_amdgcn_readlane(bn, wl);
+                        lk = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)bl.x, wl),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)bl.y, wl));
+                    }
                 } else {
+                    const int total = N[node] - kself;  // == sum of children's visits
                     // pv_mcts.py:120-130 under NumPy 2 promotion: float32 ops with sqrt(t)
                     // in double, or float64 throughout when the priors are float64;
                     // np.argmax: first maximum, a NaN counts as the maximum.
@@ -577,7 +657,7 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
                     if (depth < 64) path_lo = node;
                     else path_hi = node;
                 }
-                lk = LK[node];
+                if (PY) lk = LK[node];
                 s = next_state(s, meta_action(lk.y));
             }
             if (fail) break;
@@ -613,7 +693,7 @@ __global__ __launch_bounds__(kBlock) void k_select(Pool pool, Trees tr, EvalCach
             float *cv = s_hit[threadIdx.x >> 6];
             if (cache_lookup(cache, s, cv)) {  // the flush's evaluation is already known: apply it now
                 if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count,
-                                   tr.py != 0)) {
+                                   PY)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
                 }
@@ -1558,7 +1638,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     for (;;) {
         {
             TimedLaunch tl(e, kKSelect);
-            hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+            hipLaunchKernelGGL(e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
                                e->cache, e->timing ? e->d_bytes : nullptr);
         }
         if ((rc = check_launch())) return rc;
@@ -1595,7 +1675,7 @@ int uttt_search_select_async(uttt_engine_t *e) {
     int rc = 0;
     {
         TimedLaunch tl(e, kKSelect);
-        hipLaunchKernelGGL(k_select, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
+        hipLaunchKernelGGL(e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
                            e->cache, e->timing ? e->d_bytes : nullptr);
     }
     if ((rc = check_launch())) return rc;

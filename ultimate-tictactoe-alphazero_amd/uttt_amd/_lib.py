@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libuttt_engine.so")
+# UTTT_ENGINE_LIB: another in-tree build of the same C ABI (same-box A/B runs, tools/gpu_r3.sh abl)
+LIB_PATH = os.environ.get("UTTT_ENGINE_LIB") or os.path.join(PKG_ROOT, "libuttt_engine.so")
 
 UTTT_OK = 0
 ERRORS = {-1: "UTTT_ERR_ARG", -2: "UTTT_ERR_HIP", -3: "UTTT_ERR_CAPACITY", -4: "UTTT_ERR_ORDER",
