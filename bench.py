@@ -278,7 +278,7 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     # rounds enqueued before their count was known may have had no leaf (the move's last select)
     tower = [(int(n), a.elapsed_time(b)) for n, a, b in tower_events if int(n) > 0]
     st = {k: sp.kernel_stats(k) for k in ("select", "apply", "scan", "move_end", "select_levels", "select_trees",
-                                          "select_max_levels_sum")}
+                                          "select_max_levels_sum", "select_trips", "select_max_trips_sum")}
     out = {"sims": done, "elapsed": elapsed, "rows": sum(int(n) for n in rows), "nn_ms": union_ms(ivs),
            "nn_lane_sum_ms": sum(hi - lo for lo, hi in ivs), "tower": tower, "stats": st,
            "rounds": sp.rounds - rounds0, "finished": sp.finished - finished0, "conv": conv,
@@ -407,6 +407,17 @@ def conv_vmem_roofline(tower, avg_us, nn_ms):
                      "= lane-linear 16-B loads with every CU streaming (tools/diag/u_stream.hip)"}
 
 
+def chase_latency(chase):
+    """tools/diag/chase.hip's dependent-load latency at k_select's concurrency (2,048 waves, loads
+    missing the XCD's L2): the unit of the select latency model."""
+    if not chase:
+        return None
+    for c in chase["configs"]:
+        if c["waves"] == 2048 and c["loads"] == "plain" and c["span_bytes"] >= 1 << 30:
+            return {"us": c["us_mean"], "source": chase["source"]}
+    return None
+
+
 def hbm_roofline(name, stat, trees_per_launch, pmc_name=None):
     ms, launches, byts = stat["ms"], max(stat["launches"], 1), stat["bytes"]
     achieved = (byts / 1e9) / (ms / 1e3) if ms > 0 else 0.0
@@ -512,7 +523,9 @@ def main():
         sel_launches = max(sel["launches"], 1)
         lev_trees = max(st["select_trees"]["bytes"], 1)
         max_lev = st["select_max_levels_sum"]["bytes"] / sel_launches
+        max_trips = st["select_max_trips_sum"]["bytes"] / sel_launches
         sel_us = sel["ms"] * 1e3 / sel_launches
+        chase = newest_profile("chase.json", {})
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -553,9 +566,18 @@ def main():
                                         "levels_per_tree_per_launch": round(st["select_levels"]["bytes"] / lev_trees, 2),
                                         "slowest_tree_levels_per_launch": round(max_lev, 1),
                                         "us_per_level_of_slowest_tree": round(sel_us / max(max_lev, 1e-9), 3),
+                                        "trips_per_tree_per_launch": round(st["select_trips"]["bytes"] / lev_trees, 2),
+                                        "slowest_tree_trips_per_launch": round(max_trips, 1),
+                                        "us_per_trip_of_slowest_tree": round(sel_us / max(max_trips, 1e-9), 3),
+                                        "dependent_load_us": chase_latency(chase),
+                                        "predicted_launch_us": (round(max_trips * chase_latency(chase)["us"], 1)
+                                                                if chase else None),
                                         "note": "a launch lasts as long as its slowest tree's chain of dependent "
-                                                "levels (node header -> child stats -> next node); us_per_level is "
-                                                "the launch time divided by that chain"}),
+                                                "memory round trips (per descent the root's link and visits, one per "
+                                                "64-lane child-scan group, per completion in place the cache probe, "
+                                                "payload, re-check, path update and fence); predicted = that chain x "
+                                                "the dependent-load latency of tools/diag/chase.hip (2,048 waves, "
+                                                "random 256-B loads that miss L2)"}),
             "roofline_backup": hbm_roofline("k_apply (expand + backup, one wave per pending leaf)", st["apply"],
                                             r["trees_per_launch"], "pmc_apply.json"),
             "nn": {"rows_evaluated": r["rows"], "ms": round(r["nn_ms"], 2),

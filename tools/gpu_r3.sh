@@ -61,6 +61,10 @@ for s in $STEPS; do
                done
              done
            done ;;
+    smallpf) timeout -k 10 300 python -u tools/diag/conv_small_pf.py > $OUT/conv_small_pf.log 2>&1 ;;
+    split) timeout -k 10 300 python -u tools/diag/conv_split_time.py ${SPLIT_BOARDS:-} > $OUT/conv_split.log 2>&1 ;;
+    chase) # dependent-load latency (k_select's latency-model unit); the bench reads profiles/r*/chase.json
+           timeout -k 10 180 tools/diag/chase 200 > $OUT/chase.json && cp $OUT/chase.json profiles/r3/chase.json ;;
     bench) timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 ;;
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/prof_bench.log 2>&1 ;;

@@ -66,7 +66,10 @@ enum KernelId {
     // select latency telemetry (counters only, no launches): dependent tree levels walked
     // (sum over trees of sum over descents of depth + 1), trees that descended, the current
     // launch's slowest tree (folded into the sum by k_scan after every select), that sum
-    kKSelLevels, kKSelTrees, kKSelMax, kKSelMaxSum, kKernelCount
+    kKSelLevels, kKSelTrees, kKSelMax, kKSelMaxSum,
+    // dependent memory round trips (the latency model's unit): sum over trees, the current launch's
+    // slowest tree, that slowest count summed over launches
+    kKSelTrips, kKSelTripMax, kKSelTripMaxSum, kKernelCount
 };
 
 struct TreeCtl {
@@ -534,7 +537,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     if (t >= tr.n_trees) return;
     TreeCtl ctl = tr.ctl[t];
     int pend = 0;
-    unsigned long long bytes = 0, levels = 0;
+    unsigned long long bytes = 0;
+    unsigned int levels = 0;
+    // dependent round trips of this wave: the control loads, then per descent the root's link and visits,
+    // one per child-scan group, and for a completion in place the cache probe, payload and re-check,
+    // the path's read-modify-write and the fence
+    unsigned int trips = 1;
     if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
         const size_t base = (size_t)t * pool.cap;
         int32_t *__restrict__ N = pool.n + base;
@@ -550,6 +558,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             int path_lo = 0, path_hi = 0;  // lane d: path[d], path[64 + d]
             uint2 lk = LK[0];
             int node_n = N[0];  // the current node's visits (below the root: from the parent's scan)
+            ++trips;
             bool fail = false;
             for (;;) {
                 const int cnt = PY ? meta_L(lk.y) : meta_k(lk.y) * meta_L(lk.y);
@@ -569,6 +578,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // with it, so the winner's are read from its lane's registers instead of from
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
+                        ++trips;
                         int cn[kScanGroup];
                         float cw[kScanGroup], cp[kScanGroup];
                         uint2 cl[kScanGroup];
@@ -610,6 +620,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     }
                 } else {
                     const int total = N[node] - kself;  // == sum of children's visits
+                    trips += 2u + (unsigned int)((cnt + kWave - 1) / kWave);  // N[node], the scan, LK[node]
                     // pv_mcts.py:120-130 under NumPy 2 promotion: float32 ops with sqrt(t)
                     // in double, or float64 throughout when the priors are float64;
                     // np.argmax: first maximum, a NaN counts as the maximum.
@@ -661,7 +672,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 s = next_state(s, meta_action(lk.y));
             }
             if (fail) break;
-            levels += (unsigned long long)(depth + 1);
+            levels += (unsigned int)(depth + 1);
             const bool lose = is_lose(s);
             if (lose || legal_count(s) == 0u) {
                 // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
@@ -678,6 +689,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     N[path_hi] += 1;
                 }
                 wave_memory_fence();
+                trips += 2;
                 bytes += 16ull * (unsigned long long)(depth + 1);
                 ++sims_done;
                 if (sims_done >= tr.sims) break;
@@ -691,7 +703,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             // k = the copies the reference would queue before flushing (:127).
             const int k = min(tr.batch, tr.sims - sims_done);
             float *cv = s_hit[threadIdx.x >> 6];
+            trips += cache.flag ? 1 : 0;
             if (cache_lookup(cache, s, cv)) {  // the flush's evaluation is already known: apply it now
+                trips += 4;
                 if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count,
                                    PY)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
@@ -732,9 +746,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
         tr.pending[t] = pend;
         if (stats && bytes) atomicAdd(stats + kKSelect, bytes);
         if (stats && levels) {
-            atomicAdd(stats + kKSelLevels, levels);
+            atomicAdd(stats + kKSelLevels, (unsigned long long)levels);
             atomicAdd(stats + kKSelTrees, 1ull);
-            atomicMax(stats + kKSelMax, levels);
+            atomicMax(stats + kKSelMax, (unsigned long long)levels);
+            atomicAdd(stats + kKSelTrips, (unsigned long long)trips);
+            atomicMax(stats + kKSelTripMax, (unsigned long long)trips);
         }
     }
 }
@@ -747,6 +763,8 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     if (stats && tid == 0) {  // the select launch before this scan is complete: fold its slowest tree
         stats[kKSelMaxSum] += stats[kKSelMax];
         stats[kKSelMax] = 0ull;
+        stats[kKSelTripMaxSum] += stats[kKSelTripMax];
+        stats[kKSelTripMax] = 0ull;
     }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);

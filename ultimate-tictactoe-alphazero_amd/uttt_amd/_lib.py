@@ -19,7 +19,8 @@ ERRORS = {-1: "UTTT_ERR_ARG", -2: "UTTT_ERR_HIP", -3: "UTTT_ERR_CAPACITY", -4: "
 
 KERNELS = {"select": 0, "apply": 1, "encode": 2, "scan": 3, "move_end": 4, "hash_eval": 5,
            # select latency counters (their value is in "bytes"; no launches)
-           "select_levels": 6, "select_trees": 7, "select_max_levels_sum": 9}
+           "select_levels": 6, "select_trees": 7, "select_max_levels_sum": 9,
+           "select_trips": 10, "select_max_trips_sum": 12}
 
 
 class UtttState(ctypes.Structure):
@@ -104,6 +105,7 @@ SIGNATURES = {
     "uttt_nn_conv3x3_wino3h_dev": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, _P, _P, _P, _I32, _P, _P, _I32, _P, _I32,
                                                   _P]),
     "uttt_nn_amax": (ctypes.c_int, [_P, _I64, _P, _P]),
+    "uttt_nn_wino3h_set_split": (ctypes.c_int, [_I32]),
 }
 
 _lib = None
