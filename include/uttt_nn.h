@@ -76,6 +76,9 @@ int uttt_nn_conv3x3_wino3h_dev(const float *x, const uint16_t *u, float u_scale,
                                const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
                                uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
                                int32_t max_boards, void *stream);
+/* Small batches: the conv's 128 output channels split over 2 workgroups per set (same output bits
+ * as the persistent kernel). split: -1 automatic (default: up to 28 boards), 0 or 1 never, 2 always. */
+int uttt_nn_wino3h_set_split(int32_t split);
 /* *amax = max(*amax, max |x[i]|) over count floats, as u32 float bits (zero *amax first). */
 int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream);
 

@@ -610,6 +610,37 @@ def test_split_f16_conv_is_batch_independent(gpu):
         assert torch.equal(yb[off:off + 64], y0), off
 
 
+def test_conv_channel_split_kernel_gives_the_same_bits(gpu):
+    """Small batches run the tower conv as k_wino3s_conv (the 128 output channels split over 2
+    workgroups per set, the transform only over slots that hold a tile): it gives output and per-board
+    max bits equal to the persistent kernel's, for batch sizes covering partial groups of 7 and partial
+    sets, plain and residual forms (and so does the automatic choice)."""
+    import torch
+    from uttt_amd.model import fold_bn, random_network
+    from uttt_amd.nnfast import conv3x3_wino3h, set_conv_split, wino3h_weights
+    net = random_network(5)
+    w, b = fold_bn(net.residual_blocks[2].conv1, net.residual_blocks[2].bn1)
+    u, su = wino3h_weights(w)
+    u, b = u.cuda(), b.cuda()
+    g = torch.Generator().manual_seed(9)
+    try:
+        for n in (1, 2, 3, 4, 5, 7, 8, 11, 14, 25, 50, 71):
+            x = torch.relu(torch.randn(n, 81, 128, generator=g)).cuda()
+            x[n // 2] *= 1e3
+            r = torch.randn(n, 81, 128, generator=g).cuda()
+            for res in (None, r):
+                set_conv_split(1)
+                ya0 = torch.zeros(n, dtype=torch.int32, device="cuda")
+                y0 = conv3x3_wino3h(x, u, su, b, res, y_amax=ya0)
+                for split in (2, -1):
+                    set_conv_split(split)
+                    ya = torch.zeros(n, dtype=torch.int32, device="cuda")
+                    y = conv3x3_wino3h(x, u, su, b, res, y_amax=ya)
+                    assert torch.equal(y, y0) and torch.equal(ya, ya0), (n, split, res is None)
+    finally:
+        set_conv_split(-1)
+
+
 # ---------------------------------------------------------------- arena path --
 def test_py_semantics_search_matches_reference_pv_mcts(gpu):
     """UTTT_SEMANTICS_PY on the engine == the reference's pv_mcts.pv_mcts_scores

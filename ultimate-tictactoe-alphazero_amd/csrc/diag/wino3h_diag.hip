@@ -162,4 +162,34 @@ int uttt_diag_wino3h_pf(const float *x, const uint16_t *u, float u_scale, const 
     return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
 }
 
+// k_wino3s_conv (the small-batch channel split) at other prefetch distances: split 2 or 4, PF 3 / 6 / 9 / 12
+int uttt_diag_wino3s(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *res, float *y,
+                     const uint32_t *x_amax, int32_t n_boards, int32_t split, int32_t pf, void *stream) {
+    using namespace wino3h;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)(n_sets(n_boards) * split));
+#define UTTT_S(SP, PFV)                                                                                             \
+    do {                                                                                                            \
+        if (res)                                                                                                    \
+            hipLaunchKernelGGL((k_wino3s_conv<true, SP, PFV>), grid, dim3(64 * (8 / SP)), 0, st, x, u, u_scale, bias, \
+                               res, y, x_amax, 1, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr);         \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_wino3s_conv<false, SP, PFV>), grid, dim3(64 * (8 / SP)), 0, st, x, u, u_scale,    \
+                               bias, nullptr, y, x_amax, 1, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); \
+    } while (0)
+    if (split == 2) {
+        if (pf == 6) UTTT_S(2, 6);
+        else if (pf == 9) UTTT_S(2, 9);
+        else if (pf == 12) UTTT_S(2, 12);
+        else UTTT_S(2, 3);
+    } else {
+        if (pf == 6) UTTT_S(4, 6);
+        else if (pf == 9) UTTT_S(4, 9);
+        else if (pf == 12) UTTT_S(4, 12);
+        else UTTT_S(4, 3);
+    }
+#undef UTTT_S
+    return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
 }  // extern "C"

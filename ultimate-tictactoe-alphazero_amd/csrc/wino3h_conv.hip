@@ -142,8 +142,25 @@ static int conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, cons
         return UTTT_ERR_ARG;
     }
     if (n_boards == 0 && clear_count == 0) return UTTT_OK;
-    const dim3 grid(wino3h::grid_size(n_boards > 0 ? n_boards : 1));
     const int pb = x_amax_per_board ? 1 : 0;
+    const int split = wino3h::split_for(n_boards > 0 ? n_boards : 1);
+    if (split > 1) {
+        const dim3 sgrid((unsigned)(wino3h::n_sets(n_boards > 0 ? n_boards : 1) * split));
+        const hipStream_t s = (hipStream_t)stream;
+#define UTTT_WINO3S(RES, SP, R)                                                                                    \
+    hipLaunchKernelGGL((wino3h::k_wino3s_conv<RES, SP>), sgrid, dim3(64 * (8 / SP)), 0, s, x, u, u_scale, bias, R, y, \
+                       x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev)
+        if (residual) UTTT_WINO3S(true, 2, residual);
+        else UTTT_WINO3S(false, 2, nullptr);
+#undef UTTT_WINO3S
+        hipError_t r = hipGetLastError();
+        if (r != hipSuccess) {
+            set_error("k_wino3s_conv launch: %s", hipGetErrorString(r));
+            return UTTT_ERR_HIP;
+        }
+        return UTTT_OK;
+    }
+    const dim3 grid(wino3h::grid_size(n_boards > 0 ? n_boards : 1));
     if (residual)
         hipLaunchKernelGGL(wino3h::k_wino3h_conv<true>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
                            bias, residual, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
@@ -175,6 +192,15 @@ int uttt_nn_conv3x3_wino3h_dev(const float *x, const uint16_t *u, float u_scale,
     }
     return conv3x3_wino3h(x, u, u_scale, bias, residual, y, x_amax, x_amax_per_board, y_amax, amax_clear, clear_count,
                           max_boards, n_dev, stream);
+}
+
+int uttt_nn_wino3h_set_split(int32_t split) {
+    if (split < -1 || split > 2) {
+        set_error("uttt_nn_wino3h_set_split: split must be -1 (automatic), 0/1 (the persistent kernel) or 2");
+        return UTTT_ERR_ARG;
+    }
+    wino3h::g_split = split;
+    return UTTT_OK;
 }
 
 int uttt_nn_amax(const float *x, int64_t count, uint32_t *amax, void *stream) {

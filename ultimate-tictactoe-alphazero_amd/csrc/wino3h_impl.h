@@ -449,7 +449,8 @@ __device__ __forceinline__ SetScale set_scale(const uint32_t *__restrict__ x_ama
 template <bool RES, int MODE>
 __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScale &sc, float u_scale, floatx4 bb4,
                                              const float *__restrict__ res, float *__restrict__ y,
-                                             uint32_t *__restrict__ y_amax, int n_boards, int tid, int lane) {
+                                             uint32_t *__restrict__ y_amax, int n_boards, int tid, int lane,
+                                             int wave_base = 0) {
     // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
     // of tile slot 16rt + (lane & 15)
     const int grp = st >> 1, h = st & 1;
@@ -468,7 +469,7 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
         const int board = GB * grp + gb;
         live[rt] = gt < GB * 9 && board < n_boards;  // not the empty slot or a board past the end
         // this lane's 4 output channels, recomputed here rather than kept live (spilled) over the loop
-        const int co4e = (fresh(tid) >> 6) * 16 + 4 * (el >> 4);
+        const int co4e = (wave_base + (fresh(tid) >> 6)) * 16 + 4 * (el >> 4);
         off[rt] = ((size_t)board * 81 + (tt / 3) * 27 + (tt % 3) * 3) * C + co4e;
         board_of[rt] = board;
         // this tile's board's V scale times su: both powers of two, so 1/x is exact
@@ -666,6 +667,99 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         lds_barrier();
         mark(g, 5, t0);
     }
+}
+
+// Small batches: k_wino3s_conv<RES, SPLIT>. A set's 128 output channels are split over SPLIT
+// workgroups of NW = 8 / SPLIT waves, each wave in the product's role (16 channels x 32 tile slots,
+// the same U fragments, V fragments, MFMA order, fold and epilogue), so every output element is
+// computed by the same instruction sequence as in k_wino3h_conv: the same bits, and a board's outputs
+// still depend on that board alone. One set per SPLIT workgroups (no persistent loop): a batch of s
+// sets runs on s x SPLIT CUs instead of s, and each CU streams 1 / SPLIT of U per chunk. Staging is
+// synchronous and covers the boards in the batch only; the transform covers only the tile slots
+// that hold a tile of such a board (the others' V columns are stale, their MFMA columns independent,
+// their results dropped by the epilogue).
+template <bool RES, int SPLIT, int PF = 3>
+__global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *__restrict__ x,
+                                                                 const uint16_t *__restrict__ u, float u_scale,
+                                                                 const float *__restrict__ bias,
+                                                                 const float *__restrict__ res, float *__restrict__ y,
+                                                                 const uint32_t *__restrict__ x_amax,
+                                                                 int x_amax_per_board, uint32_t *__restrict__ y_amax,
+                                                                 uint32_t *__restrict__ amax_clear, int clear_count,
+                                                                 int n_boards, const int32_t *__restrict__ n_dev) {
+    static_assert(SPLIT == 2 || SPLIT == 4 || SPLIT == 8, "split of the 8 channel waves");
+    constexpr int NW = 8 / SPLIT, NTS = 64 * NW;
+    __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
+    float *const sX = reinterpret_cast<float *>(smem);
+    char *const sV = smem + XP * KC * 4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int part = (int)blockIdx.x % SPLIT, st = (int)blockIdx.x / SPLIT;
+    const int wave_base = part * NW, wv = wave_base + (tid >> 6);  // the product's wave role
+    for (int i = (int)blockIdx.x * NTS + tid; i < clear_count; i += (int)gridDim.x * NTS) amax_clear[i] = 0u;
+    if (n_dev) n_boards = min(n_boards, *n_dev);
+    if (st >= n_sets(n_boards)) return;
+    const int h = st & 1, b0 = GB * (st >> 1) + 3 * h;  // first staged board
+    // tile slots holding a tile of a board in the batch (slots are tiles 32h .. 32h + 31 of the group)
+    const int group_tiles = 9 * min(n_boards - GB * (st >> 1), GB);
+    const int live_slots = min(TS, group_tiles - 32 * h);
+    const int staged = min(n_boards - b0, SB) * 81;  // staged positions of boards in the batch
+    const int co4 = wv * 16 + 4 * (lane >> 4);
+    const floatx4 bb4 = *reinterpret_cast<const floatx4 *>(bias + co4);
+    Acc S[15];
+#pragma unroll
+    for (int i = 0; i < 15; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+    const floatx2 k2 = {2.0f, 2.0f}, k4 = {4.0f, 4.0f};
+    const rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(u), 0, NP * C * C * 4, 0x00020000);
+    const int kq = lane >> 4;
+    const int voff = wv * 1024 + lane * 16;
+    const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (2 * kq)) * 16);
+    BFrag bq[PF];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, 0, voff);
+    const SetScale sc = set_scale(x_amax, x_amax_per_board, b0, n_boards);
+    for (int i = tid; i < NPAD * (KC / 4); i += NTS) {  // the zero pads of the staged layout (as the product)
+        const int j = i / (KC / 4), q = i % (KC / 4);
+        const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
+                      : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
+        reinterpret_cast<float4 *>(sX + pos * KC)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        // stage this chunk's inputs of the boards in the batch, scaled by their board's sv (as store_x)
+        for (int i = tid; i < staged * (KC / 4); i += NTS) {
+            const int q = i % (KC / 4), bp = i / (KC / 4);
+            const floatx4 t = __builtin_nontemporal_load(
+                reinterpret_cast<const floatx4 *>(x + ((size_t)b0 * 81 + bp) * C + ch * KC) + q);
+            const int kb = bp / 81, pos = bp - 81 * kb, sp = spos(kb, pos / 9, pos % 9);
+            const float sv = sc.of(kb);
+            reinterpret_cast<float4 *>(sX + sp * KC)[q] = make_float4(t.x * sv, t.y * sv, t.z * sv, t.w * sv);
+        }
+        lds_barrier();
+        for (int it = tid; it < live_slots * (KC / 2); it += NTS) transform(sV, sX, it, h);
+        lds_barrier();
+        AFrag a0 = load_a(sv_lane, 0), an;
+        floatx2 mprev[4];
+        xi_loop<0, 0, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
+        lds_barrier();  // sX and sV are rewritten by the next chunk
+    }
+    set_epilogue<RES, 0>(S, st, sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, wave_base);
+}
+
+// Channel split for a batch of n boards: -1 (default) automatic, else forced (uttt_nn_wino3h_set_split;
+// 0 or 1: the persistent kernel, 2: k_wino3s_conv<2>). Automatic: split 2 up to 28 boards (four groups
+// of 7). Round 3, isolated, same box (tools/diag/conv_split_time.py, profiles/r3/conv_split.log, plain /
+// residual us): 1 board 30.5 / 30.6 -> 22.4 / 22.5, 4-16 boards 33.4 / 36.1 -> 31.6 / 32.8, 25 boards
+// 33.8 / 36.7 -> 32.0 / 33.2, but 50 boards 33.4 / 35.8 -> 39.1 / 40.6. Splits 4 and 8 are slower at
+// every size, and a deeper U prefetch (6 to 12 points) changes nothing (tools/diag/conv_small_pf.py,
+// profiles/r3/conv_small_pf.log): a set's four chunks are a serial chain of staging, transform and
+// point GEMMs whose latency, not the U stream, sets a small launch's time.
+inline int g_split = -1;
+constexpr int kSplitMaxBoards = 28;
+static int split_for(int n_boards) {
+    if (g_split >= 0) return g_split <= 1 ? 1 : g_split;
+    return n_boards <= kSplitMaxBoards ? 2 : 1;
 }
 
 // Workgroups per launch: at most cap, cap = CUs x UTTT_WINO3H_GRID (a real number, default 1:

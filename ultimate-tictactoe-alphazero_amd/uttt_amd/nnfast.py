@@ -249,6 +249,13 @@ def wino3h_weights(w):
     return torch.from_numpy(u.view(np.int16)), su.value
 
 
+def set_conv_split(split):
+    """The tower conv's channel split for small batches (uttt_nn_wino3h_set_split): -1 automatic
+    (default: split 2 up to 28 boards), 1 the persistent kernel only, 2 forced. Every choice gives the
+    same output bits."""
+    check(_lib.load().uttt_nn_wino3h_set_split(int(split)))
+
+
 def amax(x, out=None):
     """max |x| as a (1,) int32 tensor of float bits on x's device (uttt_nn_amax)."""
     if out is None:
