@@ -72,6 +72,16 @@ enum KernelId {
     kKSelTrips, kKSelTripMax, kKSelTripMaxSum, kKernelCount
 };
 
+// Device counters are striped: counter i of a row lives in kStripes 128-byte slots, and a workgroup
+// adds into slot (blockIdx & (kStripes - 1)), so thousands of waves finishing together do not
+// serialize on one address (the host sums the slots).
+constexpr int kStripes = 32;
+constexpr int kStripeStride = 16;  // u64 per slot: 128 B
+constexpr int kRow = kStripes * kStripeStride;  // u64 per counter
+__device__ __forceinline__ unsigned long long *stripe_of(unsigned long long *row) {
+    return row + (size_t)(blockIdx.x & (kStripes - 1)) * kStripeStride;
+}
+
 struct TreeCtl {
     int32_t sims_done;
     int32_t node_count;
@@ -327,7 +337,7 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
             const uint32_t sl = (h + (h >> 29)) & c.mask;
             if (atomicCAS(c.flag + sl, 2u, 1u) == 2u) {
                 slot = (int)sl;
-                atomicAdd(c.ctr + 3, 1ull);
+                atomicAdd(stripe_of(c.ctr + 3 * kRow), 1ull);
             }
         }
     }
@@ -341,7 +351,7 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         st_agent(c.flag + slot, 2u);
-        atomicAdd(c.ctr + 2, 1ull);
+        atomicAdd(stripe_of(c.ctr + 2 * kRow), 1ull);
     }
 }
 
@@ -712,7 +722,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     break;
                 }
                 wave_memory_fence();
-                if (lane == 0) atomicAdd(cache.ctr, 1ull);
+                if (lane == 0) atomicAdd(stripe_of(cache.ctr), 1ull);
                 bytes += 20ull * (unsigned long long)(k * meta_L(LK[node].y)) + 16ull * (depth + 1);
                 sims_done += k;
                 if (sims_done >= tr.sims) break;
@@ -722,7 +732,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 }
                 continue;
             }
-            if (cache.flag && lane == 0) atomicAdd(cache.ctr + 1, 1ull);
+            if (cache.flag && lane == 0) atomicAdd(stripe_of(cache.ctr + kRow), 1ull);
             int32_t *gp = tr.path + (size_t)t * kMaxDepth;
             if (lane <= depth) gp[lane] = path_lo;
             if (lane + 64 <= depth) gp[lane + 64] = path_hi;
@@ -744,13 +754,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     }
     if (lane == 0) {
         tr.pending[t] = pend;
-        if (stats && bytes) atomicAdd(stats + kKSelect, bytes);
+        if (stats && bytes) atomicAdd(stripe_of(stats + kKSelect * kRow), bytes);
         if (stats && levels) {
-            atomicAdd(stats + kKSelLevels, (unsigned long long)levels);
-            atomicAdd(stats + kKSelTrees, 1ull);
-            atomicMax(stats + kKSelMax, (unsigned long long)levels);
-            atomicAdd(stats + kKSelTrips, (unsigned long long)trips);
-            atomicMax(stats + kKSelTripMax, (unsigned long long)trips);
+            atomicAdd(stripe_of(stats + kKSelLevels * kRow), (unsigned long long)levels);
+            atomicAdd(stripe_of(stats + kKSelTrees * kRow), 1ull);
+            atomicMax(stripe_of(stats + kKSelMax * kRow), (unsigned long long)levels);
+            atomicAdd(stripe_of(stats + kKSelTrips * kRow), (unsigned long long)trips);
+            atomicMax(stripe_of(stats + kKSelTripMax * kRow), (unsigned long long)trips);
         }
     }
 }
@@ -760,11 +770,27 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
 __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats) {
     __shared__ int sums[1024];
     const int tid = threadIdx.x;
-    if (stats && tid == 0) {  // the select launch before this scan is complete: fold its slowest tree
-        stats[kKSelMaxSum] += stats[kKSelMax];
-        stats[kKSelMax] = 0ull;
-        stats[kKSelTripMaxSum] += stats[kKSelTripMax];
-        stats[kKSelTripMax] = 0ull;
+    if (stats && tid < 64) {  // the select launch before this scan is complete: fold its slowest tree
+        // (the max over the stripes, one per lane of the first wave)
+        unsigned long long ml = 0ull, mt = 0ull;
+        if (tid < kStripes) {
+            unsigned long long *a = stats + kKSelMax * kRow + tid * kStripeStride;
+            unsigned long long *b = stats + kKSelTripMax * kRow + tid * kStripeStride;
+            ml = *a;
+            mt = *b;
+            *a = 0ull;
+            *b = 0ull;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long ol = __shfl_xor(ml, off), ot = __shfl_xor(mt, off);
+            ml = ol > ml ? ol : ml;
+            mt = ot > mt ? ot : mt;
+        }
+        if (tid == 0) {
+            stats[kKSelMaxSum * kRow] += ml;
+            stats[kKSelTripMaxSum * kRow] += mt;
+        }
     }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);
@@ -927,7 +953,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             const int copies = per_copy ? k : 1;
             const unsigned long long b = 20ull * (unsigned long long)(k * L) + 81ull * 4ull * copies + 4ull * copies +
                                          8ull + 16ull * (unsigned long long)(depth + 1);
-            atomicAdd(bytes_ctr, b);
+            atomicAdd(stripe_of(bytes_ctr), b);
         }
     }
 }
@@ -1439,7 +1465,7 @@ void drain_events(uttt_engine *e) {
     e->pending_ev.resize(keep);
 }
 
-unsigned long long *bytes_ptr(uttt_engine *e, int kid) { return e->timing ? e->d_bytes + kid : nullptr; }
+unsigned long long *bytes_ptr(uttt_engine *e, int kid) { return e->timing ? e->d_bytes + (size_t)kid * kRow : nullptr; }
 
 int check_launch() {
     hipError_t r = hipGetLastError();
@@ -1539,8 +1565,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
         (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
-        (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount)) ||
-        (rc = alloc_n(e, &e->d_cache_ctr, 4)))
+        (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount * kRow)) ||
+        (rc = alloc_n(e, &e->d_cache_ctr, 4 * kRow)))
         return fail(rc);
     if ((rc = alloc_n(e, &e->d_err, 1))) return fail(rc);
     if (hipHostMalloc((void **)&e->h_move, sizeof(int64_t) * 5, hipHostMallocDefault) != hipSuccess) {
@@ -1552,8 +1578,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         return fail(UTTT_ERR_HIP);
     }
     if (hipMemsetAsync(e->tr.ctl, 0, sizeof(TreeCtl) * max_trees, e->stream) != hipSuccess ||
-        hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount, e->stream) != hipSuccess ||
-        hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount * kRow, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4 * kRow, e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess) {
         set_error("engine init memset failed");
         return fail(UTTT_ERR_HIP);
@@ -2206,9 +2232,12 @@ int uttt_engine_cache_stats2(uttt_engine_t *e, int64_t *hits, int64_t *misses, i
                              int64_t *replacements) {
     if (!e) return UTTT_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    unsigned long long c[4];
-    HIP_TRY(hipMemcpyAsync(c, e->d_cache_ctr, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+    static thread_local unsigned long long raw[4 * kRow];
+    HIP_TRY(hipMemcpyAsync(raw, e->d_cache_ctr, sizeof(raw), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    unsigned long long c[4] = {0ull, 0ull, 0ull, 0ull};
+    for (int k = 0; k < 4; ++k)
+        for (int i = 0; i < kStripes; ++i) c[k] += raw[k * kRow + i * kStripeStride];
     if (hits) *hits = (int64_t)c[0];
     if (misses) *misses = (int64_t)c[1];
     if (inserts) *inserts = (int64_t)c[2];
@@ -2228,11 +2257,13 @@ int uttt_engine_kernel_stats(uttt_engine_t *e, int32_t kernel, double *total_ms,
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     drain_events(e);
-    unsigned long long b[kKernelCount];
-    HIP_TRY(hipMemcpy(b, e->d_bytes, sizeof(b), hipMemcpyDeviceToHost));
+    unsigned long long b[kRow];
+    HIP_TRY(hipMemcpy(b, e->d_bytes + (size_t)kernel * kRow, sizeof(b), hipMemcpyDeviceToHost));
+    unsigned long long sum = 0ull;
+    for (int i = 0; i < kStripes; ++i) sum += b[i * kStripeStride];
     if (total_ms) *total_ms = e->ms[kernel];
     if (launches) *launches = e->launches[kernel];
-    if (bytes) *bytes = (int64_t)b[kernel];
+    if (bytes) *bytes = (int64_t)sum;
     return UTTT_OK;
 }
 
@@ -2245,8 +2276,8 @@ int uttt_engine_reset_stats(uttt_engine_t *e) {
         e->ms[k] = 0.0;
         e->launches[k] = 0;
     }
-    HIP_TRY(hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount, e->stream));
-    HIP_TRY(hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount * kRow, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4 * kRow, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return UTTT_OK;
 }

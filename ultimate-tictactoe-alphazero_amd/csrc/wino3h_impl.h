@@ -450,7 +450,7 @@ template <bool RES, int MODE>
 __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScale &sc, float u_scale, floatx4 bb4,
                                              const float *__restrict__ res, float *__restrict__ y,
                                              uint32_t *__restrict__ y_amax, int n_boards, int tid, int lane,
-                                             int wave_base = 0) {
+                                             int wave_base = 0, uint32_t *s_bmax = nullptr) {
     // Y[a][b] = sum_v S[a][v] A^T[b][v]; element 4rt + r is channel 16wv + 4(lane>>4) + r
     // of tile slot 16rt + (lane & 15)
     const int grp = st >> 1, h = st & 1;
@@ -534,9 +534,25 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
             // then one atomic per (tile, wave) into its board's slot
             vmax = fmaxf(vmax, __shfl_xor(vmax, 16));
             vmax = fmaxf(vmax, __shfl_xor(vmax, 32));
-            if (el < 16 && live[rt])  // v >= 0: u32 bit order = value order
-                atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
+            if (el < 16 && live[rt]) {  // v >= 0: u32 bit order = value order
+                // s_bmax: the workgroup's maxima of its staged boards in LDS, flushed to y_amax by one
+                // thread per board after the next barrier (flush_bmax); else straight to y_amax
+                if (s_bmax) atomicMax(s_bmax + (board_of[rt] - (GB * (grp) + 3 * h)), __builtin_bit_cast(uint32_t, vmax));
+                else atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
+            }
         }
+    }
+}
+
+// After the barrier that follows a set's epilogue: one global atomic per staged board with tiles in the
+// set instead of one per (tile, wave) (72 per board; same-address global atomics serialize: round 3,
+// the engine's striped counters), and the LDS row is cleared for the next set (>= 3 barriers later).
+__device__ __forceinline__ void flush_bmax(uint32_t *s_bmax, uint32_t *__restrict__ y_amax, int b0, int n_boards,
+                                           int tid) {
+    if (tid < SB) {
+        const uint32_t m = s_bmax[tid];
+        if (m && b0 + tid < n_boards) atomicMax(y_amax + b0 + tid, m);
+        s_bmax[tid] = 0u;
     }
 }
 
@@ -569,9 +585,11 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
                                                     int clear_count, int n_boards, const int32_t *__restrict__ n_dev) {
     // sX [padded position][channel] (border = 0) then sV
     __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
+    __shared__ uint32_t s_bmax[SB];
     float *const sX = reinterpret_cast<float *>(smem);
     char *const sV = smem + XP * KC * 4;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < SB) s_bmax[tid] = 0u;  // ordered before the first epilogue by the prologue's barrier
     // zero the per-board max row a later conv of this forward accumulates into
     for (int i = (int)blockIdx.x * NT + tid; i < clear_count; i += (int)gridDim.x * NT) amax_clear[i] = 0u;
     // a device-resident board count (the engine's pending count): the grid was sized for n_boards
@@ -661,10 +679,12 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         }
         mark(g, 3, t0);
-        if (c == NCH - 1) set_epilogue<RES, MODE>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane);
+        if (c == NCH - 1)
+            set_epilogue<RES, MODE>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, 0, s_bmax);
         sc = sc_next;
         mark(g, 4, t0);
         lds_barrier();
+        if (c == NCH - 1 && y_amax) flush_bmax(s_bmax, y_amax, set_b0(g), n_boards, tid);
         mark(g, 5, t0);
     }
 }
@@ -690,9 +710,11 @@ __global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *_
     static_assert(SPLIT == 2 || SPLIT == 4 || SPLIT == 8, "split of the 8 channel waves");
     constexpr int NW = 8 / SPLIT, NTS = 64 * NW;
     __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
+    __shared__ uint32_t s_bmax[SB];
     float *const sX = reinterpret_cast<float *>(smem);
     char *const sV = smem + XP * KC * 4;
     const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < SB) s_bmax[tid] = 0u;
     const int part = (int)blockIdx.x % SPLIT, st = (int)blockIdx.x / SPLIT;
     const int wave_base = part * NW, wv = wave_base + (tid >> 6);  // the product's wave role
     for (int i = (int)blockIdx.x * NTS + tid; i < clear_count; i += (int)gridDim.x * NTS) amax_clear[i] = 0u;
@@ -744,7 +766,11 @@ __global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *_
         xi_loop<0, 0, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         lds_barrier();  // sX and sV are rewritten by the next chunk
     }
-    set_epilogue<RES, 0>(S, st, sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, wave_base);
+    set_epilogue<RES, 0>(S, st, sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, wave_base, s_bmax);
+    if (y_amax) {
+        lds_barrier();
+        flush_bmax(s_bmax, y_amax, b0, n_boards, tid);
+    }
 }
 
 // Channel split for a batch of n boards: -1 (default) automatic, else forced (uttt_nn_wino3h_set_split;
