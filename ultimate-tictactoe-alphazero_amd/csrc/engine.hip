@@ -1088,17 +1088,7 @@ __device__ void mt_seed(uint32_t *key, int32_t *pos, uint32_t seed) {
     *pos = 624;
 }
 
-__device__ uint32_t mt_next32(uint32_t *key, int32_t *pos) {
-    if (*pos >= 624) {
-        for (int i = 0; i < 624; ++i) {
-            const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1 < 624 ? i + 1 : 0] & 0x7fffffffu);
-            uint32_t v = key[i + 397 < 624 ? i + 397 : i + 397 - 624] ^ (y >> 1);
-            if (y & 1u) v ^= 0x9908b0dfu;
-            key[i] = v;
-        }
-        *pos = 0;
-    }
-    uint32_t y = key[(*pos)++];
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
@@ -1106,36 +1096,96 @@ __device__ uint32_t mt_next32(uint32_t *key, int32_t *pos) {
     return y;
 }
 
-__device__ double mt_double(uint32_t *key, int32_t *pos) {
-    const uint32_t a = mt_next32(key, pos) >> 5, b = mt_next32(key, pos) >> 6;
-    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+// The standard twist of one 624-word key by the 64 lanes of a wave. Element i reads key[i], key[i + 1]
+// (old; key[0] new for i = 623) and key[(i + 397) % 624] (old for i < 227, new beyond), so three
+// stages, [0, 227), [227, 454), [454, 624), each lane loading all its inputs before any store, run the
+// sequential loop's exact updates (a thread's 624 dependent round trips took most of k_move_end).
+__device__ void mt_twist_wave(uint32_t *key) {
+    const int lane = lane_id();
+    constexpr int lo[3] = {0, 227, 454}, hi[3] = {227, 454, 624};
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
+        uint32_t a[4], b[4], c[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = lo[st] + lane + 64 * j;
+            if (i < hi[st]) {
+                a[j] = key[i];
+                b[j] = key[i + 1 < 624 ? i + 1 : 0];
+                c[j] = key[i + 397 < 624 ? i + 397 : i + 397 - 624];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = lo[st] + lane + 64 * j;
+            if (i < hi[st]) {
+                const uint32_t y = (a[j] & 0x80000000u) | (b[j] & 0x7fffffffu);
+                uint32_t v = c[j] ^ (y >> 1);
+                if (y & 1u) v ^= 0x9908b0dfu;
+                key[i] = v;
+            }
+        }
+        wave_memory_fence();  // this stage's words before the next stage reads them (other lanes)
+    }
 }
 
 // np.add.reduce on a contiguous float64 vector (pairwise, 8 accumulators, blocks <= 128).
-__device__ double np_sum(const double *a, int n) {
+__device__ double np_sum(const double *a, int n, int stride) {
     if (n < 8) {
         double r = 0.0;
-        for (int i = 0; i < n; ++i) r += a[i];
+        for (int i = 0; i < n; ++i) r += a[i * stride];
         return r;
     }
     double r[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    for (int j = 0; j < 8; ++j) r[j] = a[j * stride];
     int i = 8;
     for (; i < n - (n % 8); i += 8)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        for (int j = 0; j < 8; ++j) r[j] += a[(i + j) * stride];
     double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res += a[i];
+    for (; i < n; ++i) res += a[i * stride];
     return res;  // n <= 81 < 128: a single pairwise block
 }
 
-// One thread per slot: the per-move tail of self_play_cpp.play (:63-92). The slot's
-// f64 policy-target row of this ply (81 doubles in HBM) is the working buffer: no
-// per-thread arrays, so nothing lives in scratch.
-__global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ ctl, unsigned long long *err) {
+// One thread per slot: the per-move tail of self_play_cpp.play (:63-92). The slot's f64
+// policy-target row is worked on in LDS (one column of 81 doubles per thread, conflict-free:
+// the threads of a wave read one row), then stored to this ply's row in HBM once; worked on in
+// HBM, every read after a store was a dependent round trip.
+__global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ ctl,
+                                                  unsigned long long *err) {
+    __shared__ double s_pt[81][64];
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= sp.slots) return;
+    // np.random.choice's random_sample (numpy legacy: two 32-bit draws, 53-bit double), drawn first by
+    // every live slot with the whole wave present: a key that runs out is twisted by all 64 lanes
+    // (mt_twist_wave), one key after another, instead of by its own thread
+    const bool in = s < sp.slots;
+    const bool draws = in && sp.slot[s].live;
+    uint32_t *key = sp.mt_key + (size_t)(in ? s : 0) * 624;
+    int32_t pos = draws ? sp.mt_pos[s] : 0;
+    uint32_t w1 = 0u, w2 = 0u;
+    if (draws && pos <= 623) w1 = mt_temper(key[pos]);
+    if (draws && pos <= 622) w2 = mt_temper(key[pos + 1]);
+    const bool tw = draws && pos >= 623;
+    for (uint64_t m = __ballot(tw); m; m &= m - 1ull) {
+        const int l = __builtin_ctzll(m);
+        mt_twist_wave(sp.mt_key + (size_t)(blockIdx.x * blockDim.x + l) * 624);
+    }
+    if (tw) {
+        if (pos == 623) {  // the first word was key[623] before the twist
+            w2 = mt_temper(key[0]);
+            pos = 1;
+        } else {
+            w1 = mt_temper(key[0]);
+            w2 = mt_temper(key[1]);
+            pos = 2;
+        }
+    } else {
+        pos += 2;
+    }
+    if (draws) sp.mt_pos[s] = pos;
+    const double u = ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
+    if (!in) return;
     if (err) {  // the asynchronous move end reports a failed tree through this word
         const uint32_t st = ctl[s].status;
         if (st & kErrMask) atomicMin(err, ((unsigned long long)s << 32) | st);
@@ -1148,7 +1198,7 @@ __global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ c
     }
     const size_t base = (size_t)s * pool.cap;
     const int ply = sl.ply;
-    double *pt = sp.ply_policy + ((size_t)s * kMaxPlies + ply) * 81;
+    double *const pt = &s_pt[0][threadIdx.x];  // pt[i * 64]: element i of this slot's row
     // root scores (uttt_mcts.cpp:177-192, as root_scores) as f32 values held exactly in pt[0..L)
     int first;
     const int L = root_children(pool, base, first);
@@ -1162,7 +1212,7 @@ __global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ c
                 mi = i;
             }
         }
-        for (int i = 0; i < L; ++i) pt[i] = (i == mi) ? 1.0 : 0.0;
+        for (int i = 0; i < L; ++i) pt[(i) * 64] = (i == mi) ? 1.0 : 0.0;
     } else {
         const double y = (double)(1.0f / sp.temperature);  // glibc powf: double pow, one rounding
         float sum = 0.0f;
@@ -1170,15 +1220,15 @@ __global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ c
             // pow(x, 1) == x exactly (IEEE 754): the self-play temperature 1.0 skips the call
             const double xn = (double)pool.n[base + first + i];
             const float v = (float)(y == 1.0 ? xn : pow(xn, y));
-            pt[i] = (double)v;
+            pt[(i) * 64] = (double)v;
             sum += v;
         }
         if (sum > 0)
-            for (int i = 0; i < L; ++i) pt[i] = (double)((float)pt[i] / sum);
+            for (int i = 0; i < L; ++i) pt[(i) * 64] = (double)((float)pt[(i) * 64] / sum);
     }
     // scores -> float64, renormalised with np.sum (:74-78)
-    const double tot = np_sum(pt, L);
-    for (int i = 0; i < L; ++i) pt[i] = (tot == 0.0) ? 1.0 / (double)L : pt[i] / tot;
+    const double tot = np_sum(pt, L, 64);
+    for (int i = 0; i < L; ++i) pt[(i) * 64] = (tot == 0.0) ? 1.0 / (double)L : pt[(i) * 64] / tot;
     // policy target (:81-83): entry i moves to its action (the i-th legal action >= i, so a
     // descending scatter never overwrites an entry it still has to move), the rest are zero
     uint32_t m[3];
@@ -1188,25 +1238,23 @@ __global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ c
         for (int w = 2; w >= 0; --w)
             for (int b = 26; b >= 0; --b)
                 if ((m[w] >> b) & 1u) {
-                    pt[27 * w + b] = pt[i];
+                    pt[(27 * w + b) * 64] = pt[(i) * 64];
                     --i;
                 }
         for (int a = 0; a < 81; ++a)
-            if (!((m[a / 27] >> (a % 27)) & 1u)) pt[a] = 0.0;
+            if (!((m[a / 27] >> (a % 27)) & 1u)) pt[(a) * 64] = 0.0;
     }
     // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right.
     // Two passes over the legal actions in order, the same additions in the same order.
     double last = 0.0;
     for (int w = 0; w < 3; ++w)
-        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) last += pt[27 * w + __builtin_ctz(bits)];
-    uint32_t *key = sp.mt_key + (size_t)s * 624;
-    const double u = mt_double(key, sp.mt_pos + s);
+        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) last += pt[(27 * w + __builtin_ctz(bits)) * 64];
     int action = -1, final_action = -1;
     double acc = 0.0;
     for (int w = 0; w < 3 && action < 0; ++w)
         for (uint32_t bits = m[w]; bits; bits &= bits - 1u) {
             const int a = 27 * w + __builtin_ctz(bits);
-            acc += pt[a];
+            acc += pt[(a) * 64];
             final_action = a;
             if (!(acc / last <= u)) {
                 action = a;
@@ -1214,6 +1262,8 @@ __global__ void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ c
             }
         }
     if (action < 0) action = final_action;  // idx >= L -> L - 1
+    double *const row = sp.ply_policy + ((size_t)s * kMaxPlies + ply) * 81;
+    for (int a = 0; a < 81; ++a) row[a] = pt[a * 64];
     sp.ply_state[(size_t)s * kMaxPlies + ply] = sl.state;
     sp.ply_action[(size_t)s * kMaxPlies + ply] = (int8_t)action;
     sl.state = next_state(sl.state, action);

@@ -90,11 +90,18 @@ UTTT_HD uttt_state_t next_state(const uttt_state_t &s, int a) {
         n.opp[i] = s.own[i];
     }
     uint32_t mown = main_opp(s), mopp = main_own(s);
-    n.opp[w] |= 1u << (a % 27);
-    const uint32_t eb = cells_of(n.opp[w], b);
+    // word w chosen by selects, not a dynamic index into the local arrays (which the device
+    // compiler may place in scratch)
+    const uint32_t bit = 1u << (a % 27);
+    n.opp[0] |= w == 0 ? bit : 0u;
+    n.opp[1] |= w == 1 ? bit : 0u;
+    n.opp[2] |= w == 2 ? bit : 0u;
+    const uint32_t opp_w = w == 0 ? n.opp[0] : (w == 1 ? n.opp[1] : n.opp[2]);
+    const uint32_t own_w = w == 0 ? n.own[0] : (w == 1 ? n.own[1] : n.own[2]);
+    const uint32_t eb = cells_of(opp_w, b);
     if (win9(eb)) {
         mopp |= 1u << b;
-    } else if ((cells_of(n.own[w], b) | eb) == kCells) {
+    } else if ((cells_of(own_w, b) | eb) == kCells) {
         mown |= 1u << b;
         mopp |= 1u << b;
     }
