@@ -164,6 +164,9 @@ int uttt_search_apply(uttt_engine_t *eng, const float *policy, int64_t policy_ld
 /* Deterministic hash evaluator on device (test / micro-benchmark evaluator;
  * DESIGN.md "Hash evaluator"): n rows of nn_input -> policy (n,81), value (n). */
 int uttt_eval_hash(uttt_engine_t *eng, const float *nn_input, int32_t n, float *policy, float *value);
+/* The same evaluator on the round's pending leaves read from their states, the count read on the
+ * device (after uttt_search_select_async): rows [0, count) of policy (81 f32 each) and value. */
+int uttt_eval_hash_dev(uttt_engine_t *eng, float *policy, float *value);
 
 /* Root results after the search: visit counts of the root's children (legal
  * order, row stride 81) and |legal| per tree. */

@@ -1017,6 +1017,35 @@ __device__ void root_scores(const Pool &pool, size_t base, float temperature, fl
     }
 }
 
+// The same evaluator on this round's pending leaves straight from their states (the device-count
+// rounds: no NCHW input is written): bit j = ch * 81 + R * 9 + C of the network input, as k_encode
+// writes it, so the words and outputs are k_hash_eval's. One wave per slot; the count is read on the
+// device (the grid covers every tree).
+__global__ __launch_bounds__(kBlock) void k_hash_leaves(Trees tr, float *__restrict__ policy,
+                                                        float *__restrict__ value) {
+    const int lane = lane_id();
+    const int row = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (row >= tr.count[0]) return;
+    const uttt_state_t s = tr.leaf[tr.tree_of[row]];
+    uint32_t m[3];
+    legal_mask(s, m);
+    uint64_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = i * 64 + lane;
+        bool on = false;
+        if (j < 243) {
+            const int ch = j / 81, a = action_at(j % 81);
+            on = (ch == 0 ? bit_of(s.own, a) : (ch == 1 ? bit_of(s.opp, a) : bit_of(m, a))) != 0u;
+        }
+        w[i] = __ballot(on);
+    }
+    const uint64_t h = hash_words(w);
+    policy[(size_t)row * 81 + lane] = hash_prior(h, lane);
+    if (lane < 17) policy[(size_t)row * 81 + 64 + lane] = hash_prior(h, 64 + lane);
+    if (lane == 0) value[row] = hash_value(h);
+}
+
 __global__ void k_root_visits(Pool pool, Trees tr, int32_t *visits, int32_t *n_legal) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= tr.n_trees * 81) return;
@@ -1893,6 +1922,17 @@ int uttt_eval_hash(uttt_engine_t *e, const float *nn_input, int32_t n, float *po
     {
         TimedLaunch tl(e, kKHash);
         hipLaunchKernelGGL(k_hash_eval, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, nn_input, n, policy, value);
+    }
+    return check_launch();
+}
+
+int uttt_eval_hash_dev(uttt_engine_t *e, float *policy, float *value) {
+    if (!e || !policy || !value) return UTTT_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    {
+        TimedLaunch tl(e, kKHash);
+        hipLaunchKernelGGL(k_hash_leaves, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->tr, policy,
+                           value);
     }
     return check_launch();
 }

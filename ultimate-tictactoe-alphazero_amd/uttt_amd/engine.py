@@ -156,6 +156,12 @@ class Engine:
         check(self.lib.uttt_search_apply(self.h, ctypes.c_void_p(policy.data_ptr()), policy.stride(0),
                                          ctypes.c_void_p(value.data_ptr()), vld, int(per_copy), 1))
 
+    def eval_hash_dev(self, policy, value):
+        """The hash evaluator on the round's pending leaves (states on the device, count on the
+        device: rounds enqueued with select_async)."""
+        check(self.lib.uttt_eval_hash_dev(self.h, ctypes.c_void_p(policy.data_ptr()),
+                                          ctypes.c_void_p(value.data_ptr())))
+
     def eval_hash(self, nn_input, n, policy, value):
         check(self.lib.uttt_eval_hash(self.h, ctypes.c_void_p(nn_input.data_ptr()), int(n),
                                       ctypes.c_void_p(policy.data_ptr()), ctypes.c_void_p(value.data_ptr())))

@@ -27,7 +27,11 @@ def _bucket(n, cap, quantum=256):
 
 
 class HashEvaluator:
-    """Device hash evaluator (bit-reproducible; the parity and kernel-bench evaluator)."""
+    """Device hash evaluator (bit-reproducible; the parity and kernel-bench evaluator). With a
+    RoundCount for n (device-count rounds) it reads the pending leaves' states and the count on the
+    device (Engine.eval_hash_dev), so SelfPlay pipelines its rounds as with the fused network."""
+
+    device_count = True
 
     def __init__(self, engine):
         self.engine = engine
@@ -36,6 +40,9 @@ class HashEvaluator:
         self.value = torch.zeros((engine.max_trees, 1), dtype=torch.float32, device=dev)
 
     def __call__(self, x, n):
+        if isinstance(n, RoundCount):
+            self.engine.eval_hash_dev(self.policy, self.value)
+            return self.policy, self.value
         self.engine.eval_hash(x, n, self.policy, self.value)
         return self.policy[:n], self.value[:n]
 
