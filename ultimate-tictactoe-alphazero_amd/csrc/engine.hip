@@ -766,9 +766,37 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
 }
 
 // ------------------------------------------------------------------- scan --
+// Exclusive prefix sum of one value per thread over a 1,024-thread block (16 waves): a wave scan
+// by lane shifts, the 16 wave totals scanned by the first wave through LDS; two barriers where
+// a Hillis-Steele scan over LDS takes twenty. Returns the exclusive prefix; *total gets the sum.
+template <typename T>
+__device__ __forceinline__ T block_scan_1024(T v, T *total, T *wsum /* __shared__ [16] */) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    T x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T t = __shfl_up(x, off);
+        if (lane >= off) x += t;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        T w = lane < 16 ? wsum[lane] : T(0);
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const T t = __shfl_up(w, off);
+            if (lane >= off) w += t;
+        }
+        if (lane < 16) wsum[lane] = w;
+    }
+    __syncthreads();
+    *total = wsum[15];
+    return x - v + (wave > 0 ? wsum[wave - 1] : T(0));
+}
+
 // One block: exclusive scan of pending flags -> tree_of[slot] in tree order.
 __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats) {
-    __shared__ int sums[1024];
+    __shared__ unsigned long long wsum[16];
     const int tid = threadIdx.x;
     if (stats && tid < 64) {  // the select launch before this scan is complete: fold its slowest tree
         // (the max over the stripes, one per lane of the first wave)
@@ -794,35 +822,23 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);
-    __shared__ int capped, more;
-    if (tid == 0) capped = more = 0;
-    int local = 0, cap = 0, mo = 0;
+    unsigned long long local = 0, cap = 0, mo = 0;
     for (int i = b; i < e; ++i) {
         const int p = tr.pending[i];
         local += p == 1 || p == 3;
         cap += p == 2;
         mo += p >= 2;
     }
-    sums[tid] = local;
-    __syncthreads();
-    if (cap) atomicAdd(&capped, cap);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mo += __shfl_xor(mo, off);  // one LDS atomic per wave
-    if ((tid & 63) == 0 && mo) atomicAdd(&more, mo);
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int v = tid >= off ? sums[tid - off] : 0;
-        __syncthreads();
-        sums[tid] += v;
-        __syncthreads();
-    }
-    int slot = sums[tid] - local;
+    // the three counts in 21-bit fields of one scanned word (each total <= n_trees < 2^21)
+    unsigned long long tot;
+    const unsigned long long ex = block_scan_1024(local | (cap << 21) | (mo << 42), &tot, wsum);
+    int slot = (int)(ex & 0x1FFFFFull);
     for (int i = b; i < e; ++i)
         if (tr.pending[i] == 1 || tr.pending[i] == 3) tr.tree_of[slot++] = i;
-    if (tid == 1023) {
-        tr.count[0] = sums[1023];
-        tr.count[1] = capped;
-        tr.count[2] = more;  // trees with simulations left after this round (0: the search ends with it)
+    if (tid == 0) {
+        tr.count[0] = (int)(tot & 0x1FFFFFull);
+        tr.count[1] = (int)((tot >> 21) & 0x1FFFFFull);
+        tr.count[2] = (int)(tot >> 42);  // trees with simulations left after this round (0: the search ends with it)
     }
 }
 
@@ -1310,8 +1326,7 @@ __global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const T
 // One block: give finished games arena rows (slot order) and free slots the
 // next game ids (slot order) — deterministic for a given slot count.
 __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
-    __shared__ long long fin_sum[1024];
-    __shared__ int free_sum[1024];
+    __shared__ unsigned long long wsum[16];
     const int tid = threadIdx.x;
     const int per = (sp.slots + 1023) / 1024;
     const int b = tid * per, e = min(b + per, sp.slots);
@@ -1325,25 +1340,17 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
         }
         if (!sl.live) ++fr;
     }
-    fin_sum[tid] = fl;
-    free_sum[tid] = fr;
-    __shared__ int fcount[1024];
-    fcount[tid] = fc;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const long long a = tid >= off ? fin_sum[tid - off] : 0;
-        const int c = tid >= off ? free_sum[tid - off] : 0;
-        const int d = tid >= off ? fcount[tid - off] : 0;
-        __syncthreads();
-        fin_sum[tid] += a;
-        free_sum[tid] += c;
-        fcount[tid] += d;
-        __syncthreads();
-    }
+    unsigned long long fl_tot, cnt_tot;
+    const unsigned long long fl_ex = block_scan_1024((unsigned long long)fl, &fl_tot, wsum);
+    __syncthreads();  // wsum is reused
+    const unsigned long long cnt_ex =
+        block_scan_1024((unsigned long long)fr | ((unsigned long long)fc << 32), &cnt_tot, wsum);
     const int64_t arena0 = sp.ctr[2], games0 = sp.ctr[1], next0 = sp.ctr[0];
-    long long off = arena0 + fin_sum[tid] - fl;
-    int gi = (int)(games0 + fcount[tid] - fc);
-    int fi = free_sum[tid] - fr;
+    long long off = arena0 + (long long)fl_ex;
+    int gi = (int)(games0 + (long long)(cnt_ex >> 32));
+    int fi = (int)(cnt_ex & 0xFFFFFFFFull);
+    const long long fin_total = (long long)fl_tot;
+    const int free_total = (int)(cnt_tot & 0xFFFFFFFFull), fin_count = (int)(cnt_tot >> 32);
     for (int i = b; i < e; ++i) {
         Slot sl = sp.slot[i];
         if (sl.finished) {
@@ -1379,14 +1386,14 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
         sp.live[i] = sl.live;
         sp.slot[i] = sl;
     }
-    __syncthreads();
-    if (tid == 1023) {
-        sp.ctr[2] = arena0 + fin_sum[1023];
-        sp.ctr[1] = games0 + fcount[1023];
-        const int64_t nxt = next0 + free_sum[1023];
+    __syncthreads();  // every thread read sp.ctr before it is rewritten
+    if (tid == 0) {
+        sp.ctr[2] = arena0 + fin_total;
+        sp.ctr[1] = games0 + fin_count;
+        const int64_t nxt = next0 + free_total;
         sp.ctr[0] = nxt < sp.game_end ? nxt : sp.game_end;
         // live slots for the next move: those still playing plus the free ones given a game
-        sp.ctr[3] = (int64_t)(sp.slots - free_sum[1023]) + (sp.ctr[0] - next0);
+        sp.ctr[3] = (int64_t)(sp.slots - free_total) + (sp.ctr[0] - next0);
     }
 }
 
@@ -1601,8 +1608,10 @@ extern "C" {
 const char *uttt_version(void) { return "uttt-mi355x 0.1 (gfx950)"; }
 
 int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out) {
-    if (!out || max_trees <= 0 || max_sims <= 0 || max_sims > 60000) {
-        set_error("uttt_engine_create: bad arguments (max_trees=%d, max_sims=%d)", max_trees, max_sims);
+    if (!out || max_trees <= 0 || max_trees >= (1 << 21) || max_sims <= 0 || max_sims > 60000) {
+        // (k_scan packs its three per-round counts into 21-bit fields)
+        set_error("uttt_engine_create: bad arguments (max_trees=%d of at most 2097151, max_sims=%d)", max_trees,
+                  max_sims);
         return UTTT_ERR_ARG;
     }
     int ndev = 0;
