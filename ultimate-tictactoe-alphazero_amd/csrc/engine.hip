@@ -393,8 +393,10 @@ __device__ float np_sum_f32_legal(float p0, float p1, uint64_t b0, uint64_t b1, 
     return res;
 }
 
+// raw0 / raw1: this lane's prior of action lane / 64 + lane (lane < 17), loaded by the caller
 __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi, int k,
-                              const uttt_state_t &s, const float *pol, float v, int &node_count, bool py = false) {
+                              const uttt_state_t &s, float raw0, float raw1, float v, int &node_count,
+                              bool py = false) {
     const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
@@ -407,8 +409,8 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     if ((int64_t)nb + (int64_t)blocks * L > pool.cap || L == 0) return false;
     const int i0 = __popcll(b0 & lanes_below());
     const int i1 = __popcll(b0) + __popcll(b1 & lanes_below());
-    const float p0 = l0 ? pol[lane] : 0.0f;
-    const float p1 = l1 ? pol[64 + lane] : 0.0f;
+    const float p0 = l0 ? raw0 : 0.0f;
+    const float p1 = l1 ? raw1 : 0.0f;
     float sum = 0.0f;
     if (py) {
         sum = np_sum_f32_legal(p0, p1, b0, b1, L);
@@ -716,7 +718,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             trips += cache.flag ? 1 : 0;
             if (cache_lookup(cache, s, cv)) {  // the flush's evaluation is already known: apply it now
                 trips += 4;
-                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv, cv[81], ctl.node_count,
+                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv[lane], lane < 17 ? cv[64 + lane] : 0.0f,
+                                   cv[81], ctl.node_count,
                                    PY)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
@@ -874,23 +877,36 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
                                                   unsigned long long *bytes_ctr) {
     const int lane = lane_id();
     const int slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (slot >= tr.count[0]) return;
-    const int t = tr.tree_of[slot];
+    // two dependent round trips before the work: the count with this slot's tree (tree_of holds
+    // n_trees entries, stale past the count), then the tree's records, its path and the slot's
+    // evaluation, all loaded unconditionally (branch-free; masked where used)
+    const int cnt = tr.count[0];
+    const int t = tr.tree_of[slot < tr.n_trees ? slot : 0];
+    if (slot >= cnt) return;
     const LeafRec r = tr.rec[t];
     TreeCtl ctl = tr.ctl[t];
     const uttt_state_t s = tr.leaf[t];
     const size_t base = (size_t)t * pool.cap;
+    const int32_t *gp = tr.path + (size_t)t * kMaxDepth;
+    const int g_lo = gp[lane], g_hi = gp[lane + 64];
+    float raw0 = 0.0f, raw1 = 0.0f, rawv = 0.0f;
+    if (!per_copy) {
+        const float *pol = policy + (int64_t)slot * pld;
+        raw0 = pol[lane];
+        raw1 = pol[64 + (lane < 17 ? lane : 16)];
+        rawv = value[(int64_t)slot * vld];
+    }
     const int depth = r.depth;
     const int k = r.k;
-    const int32_t *gp = tr.path + (size_t)t * kMaxDepth;
-    const int pn_lo = lane <= depth ? gp[lane] : 0;
-    const int pn_hi = lane + 64 <= depth ? gp[lane + 64] : 0;
+    const int pn_lo = lane <= depth ? g_lo : 0;
+    const int pn_hi = lane + 64 <= depth ? g_hi : 0;
     int L = 0;
     const int nodes_before = ctl.node_count;
     if (!per_copy) {
         const float *pol = policy + (int64_t)slot * pld;
-        const float v = value[(int64_t)slot * vld];
-        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, pol, v, ctl.node_count, tr.py != 0)) {
+        const float v = rawv;
+        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f, v,
+                           ctl.node_count, tr.py != 0)) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;

@@ -120,7 +120,12 @@ UTTT_HD int action_at(int pos) {
     const int R = pos / 9, C = pos % 9;
     return ((R / 3) * 3 + C / 3) * 9 + (R % 3) * 3 + C % 3;
 }
-UTTT_HD uint32_t bit_of(const uint32_t w[3], int a) { return (w[a / 27] >> (a % 27)) & 1u; }
+// the word chosen by selects, not a dynamic index (which puts a local state in LDS or scratch)
+UTTT_HD uint32_t bit_of(const uint32_t w[3], int a) {
+    const int i = a / 27;
+    const uint32_t x = i == 0 ? w[0] : (i == 1 ? w[1] : w[2]);
+    return (x >> (a % 27)) & 1u;
+}
 
 // ---------------------------------------------------------------------------
 // Deterministic hash evaluator (DESIGN.md "Hash evaluator"). Input: the 243
