@@ -482,9 +482,11 @@ def main():
                         # per move, and the one-hot scores make every game play the same line, so the cache
                         # answers every leaf above; off, each move is one network call on 1,024 boards
                         ("c2_1024x50_b1024_cache_off", dict(games=1024, batch=1024, age=100, cache_log2=0)),
-                        # SURVEY §8(d) kernel microbench: the search kernels alone (hash evaluator, no network)
-                        ("tree_only_4096x50", dict(evaluator="hash", age=100)),
-                        ("tree_only_4096x400", dict(evaluator="hash", sims=400, age=30, warmup=2, steps=4))):
+                        # SURVEY §8(d) kernel microbench: the search kernels alone (hash evaluator, no network),
+                        # one lane: with no network to overlap, one launch per round over every tree is the
+                        # fastest shape (1 / 2 / 4 lanes: 170.6M / 141M / 82M sims/s, profiles/r3/ab/hashlanes.log)
+                        ("tree_only_4096x50", dict(evaluator="hash", age=100, lanes=1)),
+                        ("tree_only_4096x400", dict(evaluator="hash", sims=400, age=30, warmup=2, steps=4, lanes=1))):
             cfg = dict(net=net0, games=G, sims=S, batch=B, lanes=args.lanes, cache_log2=args.cache_log2,
                        age=args.age, warmup=3, steps=10, evaluator=args.evaluator)
             cfg.update(kw)
