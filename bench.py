@@ -498,8 +498,10 @@ def main():
             sv["net"] = "calibrated (tests/golden/netcal.npz)" if key == "calibrated_net" else args.net
             if cfg["evaluator"] == "hash":
                 sv["net"] = None
-                sv["roofline_select"] = hbm_roofline("k_select", rv["stats"]["select"], rv["trees_per_launch"])
-                sv["roofline_backup"] = hbm_roofline("k_apply", rv["stats"]["apply"], rv["trees_per_launch"])
+                sv["roofline_select"] = hbm_roofline("k_select", rv["stats"]["select"], rv["trees_per_launch"],
+                                                     "pmc_select_tree.json" if cfg["sims"] == S else None)
+                sv["roofline_backup"] = hbm_roofline("k_apply", rv["stats"]["apply"], rv["trees_per_launch"],
+                                                     "pmc_apply_tree.json" if cfg["sims"] == S else None)
                 sv["breakdown_ms"] = {k: round(rv["stats"][k]["ms"], 2) for k in ("select", "apply", "scan", "move_end")}
                 sv["breakdown_ms"]["evaluator"] = round(rv["nn_ms"], 2)
                 sv["breakdown_ms"]["wall"] = round(rv["elapsed"] * 1e3, 2)

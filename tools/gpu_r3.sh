@@ -23,6 +23,8 @@ for s in $STEPS; do
     cycle) timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle.json ${CYCLE_ARGS:-} > $OUT/cycle.log 2>&1 ;;
     cycle16) UTTT_TRAIN_PRECISION=f16 timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle_f16.json ${CYCLE_ARGS:-} > $OUT/cycle_f16.log 2>&1 ;;
     hist)  timeout -k 10 300 python -u tools/bench_history.py > $OUT/history.log 2>&1 ;;
+    pmctree) PMC_OUT=gpurun_out/pmc_tree PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
+               > $OUT/pmc_tree.log 2>&1 ;;
     pmcsel) timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 ;;
     pmcconv) timeout -k 10 600 bash tools/pmc_conv.sh > $OUT/pmc_conv.log 2>&1 && \
              python tools/pmc_conv_summary.py gpurun_out/pmc_conv ${N:-1344} $OUT/pmc_conv.json >> $OUT/pmc_conv.log 2>&1 ;;
