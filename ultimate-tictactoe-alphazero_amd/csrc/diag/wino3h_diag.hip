@@ -131,6 +131,7 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
         case 50: UTTT_V(kSerialPrologue, 3); break;
         case 51: UTTT_V(kSplitCvt, 3); break;
         case 52: UTTT_V(kSplitCvt | kSerialPrologue, 3); break;
+        case 60: UTTT_V(kL2Prefetch, 3); break;
         case 30: UTTT_Q(3); break;
         case 31: UTTT_Q(2); break;
         case 32: UTTT_Q(4); break;

@@ -61,6 +61,7 @@ constexpr int kFoldScalar = 1 << 24;    // ... as scalar v_add_f32 / v_fma_f32 p
 constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS latency) instead of one
 constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
+constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
 
 struct Acc {
     floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
@@ -655,10 +656,21 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     auto mark = [&](int g, int k, unsigned long long t0) {
         if (stamp && g < 8) UTTT_WINO3H_STAMP(blockIdx.x, tid >> 8, g, k, (unsigned int)(__builtin_amdgcn_s_memtime() - t0));
     };
+    uint32_t pf_sink = 0u;
 #pragma unroll 1
     for (int g = 0; g < G; ++g) {
         const int c = g % NCH, ch = chunk_of(g);
         const unsigned long long t0 = (MODE & 4) ? __builtin_amdgcn_s_memtime() : 0ull;
+        if constexpr (MODE & kL2Prefetch) {
+            // diagnostic: the previous touch is consumed here, a chunk after it was issued; then the rows
+            // of chunk g + 2 are touched with plain (L2-allocating) loads, so its nontemporal loads hit L2
+            asm volatile("" ::"v"(pf_sink));
+            if (g + 2 < G) {
+                const int b0n = set_b0(g + 2), rows = min((n_boards - b0n) * 81, SB * 81);
+                const int bp = fresh(tid);
+                if (bp < rows) pf_sink = *reinterpret_cast<const uint32_t *>(x + ((size_t)b0n * 81 + bp) * C + chunk_of(g + 2) * KC);
+            }
+        }
         // the next chunk's inputs load during this chunk's transform (registers are
         // free then; the point loop needs nearly all of them)
         if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
