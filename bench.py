@@ -476,12 +476,13 @@ def main():
         for key, kw in (("calibrated_net", dict(net=calibrated_network(NETCAL, dev))),
                         ("cache_off", dict(cache_log2=0)),
                         ("c3_4096x400", dict(sims=400, age=30, warmup=2, steps=4)),
-                        # BASELINE configs[1]: 1,024 games x 50 sims, MCTS_BATCH_SIZE 1024 (one flush per move)
-                        ("c2_1024x50_b1024", dict(games=1024, batch=1024, age=100)),
-                        # the same without the evaluation cache: with B >= S every tree flushes one leaf
-                        # per move, and the one-hot scores make every game play the same line, so the cache
-                        # answers every leaf above; off, each move is one network call on 1,024 boards
-                        ("c2_1024x50_b1024_cache_off", dict(games=1024, batch=1024, age=100, cache_log2=0)),
+                        # BASELINE configs[1]: 1,024 games x 50 sims, MCTS_BATCH_SIZE 1024 (one flush per move):
+                        # each move is one network call on 1,024 boards. Measured with the evaluation cache
+                        # OFF: with B >= S every tree flushes one leaf per move and the one-hot scores make
+                        # every game play the same line, so a cache would answer every leaf and the line
+                        # would time no network at all (that degenerate form is kept beside it, labelled)
+                        ("c2_1024x50_b1024", dict(games=1024, batch=1024, age=100, cache_log2=0)),
+                        ("c2_1024x50_b1024_cache_on_degenerate", dict(games=1024, batch=1024, age=100)),
                         # SURVEY §8(d) kernel microbench: the search kernels alone (hash evaluator, no network),
                         # one lane: with no network to overlap, one launch per round over every tree is the
                         # fastest shape (1 / 2 / 4 lanes: 170.6M / 141M / 82M sims/s, profiles/r3/ab/hashlanes.log)
@@ -496,6 +497,14 @@ def main():
             sv["config"] = {k: cfg[k] for k in ("games", "sims", "batch", "lanes", "cache_log2", "age", "steps",
                                                 "evaluator")}
             sv["net"] = "calibrated (tests/golden/netcal.npz)" if key == "calibrated_net" else args.net
+            # every line says whether its timed steps ran the network at all
+            sv["evaluates_network"] = cfg["evaluator"] != "hash" and sv["rows_per_step"] > 0
+            if key.endswith("_degenerate"):
+                sv["degenerate"] = True
+                sv["note"] = ("configs[1] with the evaluation cache on: B >= S gives one flush per tree per move and "
+                              "one-hot scores, every game plays the same line and the cache answers every leaf, so "
+                              "this line times the search kernels only (rows_per_step 0); variants.c2_1024x50_b1024 "
+                              "(cache off) is the configs[1] measurement")
             if cfg["evaluator"] == "hash":
                 sv["net"] = None
                 sv["roofline_select"] = hbm_roofline("k_select", rv["stats"]["select"], rv["trees_per_launch"],
@@ -529,7 +538,7 @@ def main():
         max_lev = st["select_max_levels_sum"]["bytes"] / sel_launches
         max_trips = st["select_max_trips_sum"]["bytes"] / sel_launches
         sel_us = sel["ms"] * 1e3 / sel_launches
-        chase = newest_profile("chase.json", {})
+        chase_lat = chase_latency(newest_profile("chase.json", {}))
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -573,9 +582,9 @@ def main():
                                         "trips_per_tree_per_launch": round(st["select_trips"]["bytes"] / lev_trees, 2),
                                         "slowest_tree_trips_per_launch": round(max_trips, 1),
                                         "us_per_trip_of_slowest_tree": round(sel_us / max(max_trips, 1e-9), 3),
-                                        "dependent_load_us": chase_latency(chase),
-                                        "predicted_launch_us": (round(max_trips * chase_latency(chase)["us"], 1)
-                                                                if chase else None),
+                                        "dependent_load_us": chase_lat,
+                                        "predicted_launch_us": (round(max_trips * chase_lat["us"], 1)
+                                                                if chase_lat else None),
                                         "note": "a launch lasts as long as its slowest tree's chain of dependent "
                                                 "memory round trips (per descent the root's link and visits, one per "
                                                 "64-lane child-scan group, per completion in place the cache probe, "

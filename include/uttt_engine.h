@@ -36,6 +36,7 @@ extern "C" {
 #define UTTT_ERR_CAPACITY (-3) /* node pool / path / record arena exhausted         */
 #define UTTT_ERR_ORDER (-4)    /* call out of sequence (e.g. apply before select)   */
 #define UTTT_ERR_NODEVICE (-5) /* no gfx950 device / device ordinal out of range    */
+#define UTTT_ERR_NONFINITE (-6) /* evaluator returned NaN/Inf (legal prior or value) */
 
 #define UTTT_ACTIONS 81
 #define UTTT_INPUT_SIZE 243 /* (3, 9, 9) NCHW f32 per position */

@@ -472,6 +472,83 @@ def test_eval_cache_is_exact(gpu, oracle_lib):
     assert st["hits"] > 0 and st["inserts"] > 0
 
 
+def test_nonfinite_evaluator_output_is_refused(gpu, oracle_lib):
+    """SURVEY §5 failure detection. A NaN value or an Inf legal prior from the evaluator stops its
+    tree (the reference would back it up silently, uttt_mcts.cpp:144-166) and the search end raises
+    UTTT_ERR_NONFINITE; the poisoned row is neither expanded nor cached, so a later search with the
+    same table and a clean evaluator matches the oracle bit for bit."""
+    from uttt_amd._lib import EngineError
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 64, seed=31)
+    bs = gpu.BatchedSearch(len(roots), 400, cache_log2=14)
+    ev = gpu.HashEvaluator(bs.engine)
+
+    class Poison:
+        def __init__(self, kind):
+            self.kind, self.calls = kind, 0
+
+        def __call__(self, x, n):
+            p, v = ev(x, n)
+            self.calls += 1
+            if self.calls == 3:
+                p, v = p.clone(), v.clone()
+                if self.kind == "value":
+                    v[n // 2] = float("nan")
+                else:
+                    p[n // 2, :] = float("inf")
+            return p, v
+
+    for kind in ("value", "policy"):
+        with pytest.raises(EngineError, match="NONFINITE"):
+            bs.run(roots, Poison(kind), 50, 8)
+            bs.scores(1.0)
+    inserts = bs.engine.cache_stats()["inserts"]
+    assert inserts > 0
+    bs.run(roots, ev, 50, 8)
+    visits, L = bs.visits()
+    for i, s in enumerate(ostates):
+        _, vi, _ = core.pv_mcts_scores_hash(s, 1.0, 50, 8)
+        assert np.array_equal(visits[i, :L[i]], vi), i
+    assert bs.engine.cache_stats()["hits"] > 0
+
+
+def test_nonfinite_in_async_selfplay_leaves_the_move_unended(gpu, oracle_lib):
+    """Self-play with device-count rounds and asynchronous move ends: a NaN value stops its tree,
+    the move end that follows changes nothing (k_tree_err, then k_move_end / k_finalize / k_archive
+    skip), and the host raises UTTT_ERR_NONFINITE when it reads that move's result. Every game
+    archived before the failure equals the oracle's."""
+    import torch
+    from uttt_amd._lib import EngineError
+    core = oracle_lib
+    n_games, seed = 12, 4242
+
+    class PoisonDev:
+        device_count = True
+
+        def __init__(self, eng):
+            self.h = gpu.HashEvaluator(eng)
+            self.calls = 0
+
+        def __call__(self, x, n):
+            p, v = self.h(x, n)
+            self.calls += 1
+            if self.calls >= 700:  # some games have been archived by then
+                v.fill_(float("nan"))
+            return p, v
+
+    sp = gpu.SelfPlay(4, 30, 4, 1.0)
+    sp.set_evaluator(PoisonDev)
+    with pytest.raises(EngineError, match="NONFINITE"):
+        sp.run(0, n_games, seed)
+    torch.cuda.synchronize()
+    recs = sp.records()
+    assert 0 < len(recs) < n_games
+    for r in recs:
+        ref = core.self_play_game_hash(seed + r["game"], 1.0, 30, 4)
+        assert np.array_equal(r["actions"], ref["actions"].astype(np.int64)), r["game"]
+        assert np.array_equal(r["policies"].view(np.uint64), ref["policies"].view(np.uint64))
+
+
 def test_split_f16_winograd_conv_matches_f64(gpu):
     """The split-f16 F(3x3,3x3) kernel (wino3h) vs an f64 direct conv: within 1e-5 of each
     board's output scale (the bar the f32 kernels meet) for ragged board counts (partial last

@@ -42,3 +42,30 @@ def test_fast_history_on_golden_games(tmp_path):
     assert H.lists_equal(got, ref)
     for i, (xi, pi, vi) in enumerate(got):
         assert np.array_equal(pi.view(np.uint64), d["policies"][i].view(np.uint64)) and vi == int(d["values"][i])
+
+
+def test_streamed_history_chunks_equal_one_piece(tmp_path, monkeypatch):
+    """write_history_file streams ply blocks built from whole games (bounded host memory): with tiny
+    blocks, boundaries inside and between games, the file equals the one-piece writer's bytes."""
+    from uttt_amd import history as H
+    rng = np.random.RandomState(9)
+    recs = []
+    for g, n in enumerate((1, 5, 2, 9, 1, 1, 13, 4)):
+        recs.append({"inputs": (rng.rand(n, 9, 9, 3) < 0.3).astype(np.float32),
+                     "policies": rng.dirichlet(np.ones(81), size=n), "values": rng.randint(-1, 2, size=n)})
+    x = np.concatenate([r["inputs"].reshape(-1, 243) for r in recs])
+    p = np.concatenate([r["policies"] for r in recs])
+    v = np.concatenate([r["values"] for r in recs])
+    whole = H.history_bytes(x, p, v)
+    for cap in (1, 3, 7, 1 << 16):
+        monkeypatch.setattr(H, "CHUNK_PLIES", cap)
+        path = str(tmp_path / f"c{cap}.history")
+        n = H.write_history_file(recs, path)
+        with open(path, "rb") as fh:
+            got = fh.read()
+        assert n == len(got) and got == whole, cap
+        assert H.history_bytes(x, p, v) == whole
+    path = str(tmp_path / "empty.history")
+    H.write_history_file([], path)
+    with open(path, "rb") as fh:
+        assert pickle.load(fh) == []  # written by this test

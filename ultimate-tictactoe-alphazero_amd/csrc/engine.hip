@@ -59,7 +59,21 @@ constexpr int32_t kLive = 1;
 constexpr int32_t kErrCapacity = 2;
 constexpr int32_t kErrDepth = 4;
 constexpr int32_t kErrSelect = 8;
-constexpr int32_t kErrMask = kErrCapacity | kErrDepth | kErrSelect;
+constexpr int32_t kErrNonFinite = 16;  // the evaluator returned a NaN / Inf legal prior or value
+constexpr int32_t kErrMask = kErrCapacity | kErrDepth | kErrSelect | kErrNonFinite;
+
+// a failed tree's status -> message and UTTT_ERR_* (the checks that raise it are at the move / search end)
+static const char *tree_error_text(uint32_t st) {
+    return (st & kErrCapacity)    ? "node pool exhausted"
+           : (st & kErrDepth)     ? "path deeper than 128"
+           : (st & kErrNonFinite) ? "non-finite evaluator output (NaN or Inf in a legal prior or the value)"
+                                  : "no selectable child (NaN statistics)";
+}
+static int tree_error_code(uint32_t st) {
+    return (st & kErrCapacity) || (st & kErrDepth) ? UTTT_ERR_CAPACITY
+           : (st & kErrNonFinite)                  ? UTTT_ERR_NONFINITE
+                                                   : UTTT_ERR_ARG;
+}
 
 enum KernelId {
     kKSelect = 0, kKApply, kKEncode, kKScan, kKMoveEnd, kKHash,
@@ -204,14 +218,27 @@ __device__ __forceinline__ void wave_memory_fence() { __builtin_amdgcn_fence(__A
 // k_select (a hit is expanded in place: no network round), filled by k_apply.
 constexpr int kProbe = 8;
 constexpr int kCacheVal = 82;
+// One record per slot, three 128-byte lines: the key (32 B), the 82 values (328 B), padding. Written
+// and read as 16-byte agent-scope (sc1) accesses, 23 lanes of one wave: one fabric write per 16 B
+// instead of one per 4-byte store (MI355X_MICROARCH.md: narrow sc1 stores are one fabric write each).
+constexpr int kRecBytes = 384;
+constexpr int kRecKey = 0, kRecVal = 32;
+constexpr int kRecLanes = 23;  // 16-byte pieces written per record: 2 of key, 21 of values
+constexpr int kSc1 = 16;       // buffer-intrinsic cache-policy bit: sc1 (agent scope)
+static_assert(kRecVal + 16 * (kRecLanes - 2) >= kRecVal + 4 * kCacheVal && 16 * kRecLanes <= kRecBytes, "record");
 
 struct EvalCache {
-    uint32_t *flag;      // 0 empty, 1 claimed, 2 ready
-    uttt_state_t *key;
-    float *val;          // [slot][82]
+    // 0 empty; odd: a writer holds the slot; even >= 2: ready. A writer claims by CAS from the value it
+    // saw to that + 1 and publishes that + 2, so every publish is a new version: a reader compares the
+    // flag it probed with the flag after its copy (a seqlock without ABA).
+    uint32_t *flag;
+    char *rec;           // [slot][kRecBytes]
     uint32_t mask;       // capacity - 1
     unsigned long long *ctr;  // [0] hits, [1] misses (network leaves), [2] inserts, [3] replacements
 };
+
+__device__ __forceinline__ bool flag_ready(uint32_t f) { return f != 0u && !(f & 1u); }
+__device__ __forceinline__ uint32_t flag_next(uint32_t f) { return f + 2u == 0u ? 2u : f + 2u; }  // f even
 
 __device__ __forceinline__ uint32_t state_hash(const uttt_state_t &s) {
     const uint64_t a = ((uint64_t)s.own[1] << 32) | s.own[0];
@@ -227,12 +254,11 @@ __device__ __forceinline__ bool same_state(const uttt_state_t &x, const uttt_sta
 }
 
 // The table may be shared by several engines whose kernels run concurrently on
-// other XCDs, whose L2s are not coherent with this one: every access to flag,
-// key and val is an agent-scope atomic (sc1: served from memory, not from a
-// possibly stale L2 line). Entries are exact (the evaluator is a pure function
-// of the position), so any ready entry with a matching key is correct; a
-// reader re-checks flag and key after copying the values so an entry recycled
-// meanwhile (clear + re-insert) is never mixed into the copy.
+// other XCDs, whose L2s are not coherent with this one: every access to flag and
+// record is agent-scope (sc1: relaxed agent atomics, or buffer accesses with the
+// sc1 bit). Entries are exact (the evaluator is a pure function of the position),
+// so any ready entry with a matching key is correct; a reader re-checks the flag
+// after copying the values, so an entry rewritten meanwhile is never mixed into the copy.
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -242,18 +268,28 @@ __device__ __forceinline__ void st_agent(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// a wave-uniform slot's record as a 384-byte buffer
+__device__ __forceinline__ rsrc_t rec_rsrc(const EvalCache &c, uint32_t slot) {
+    slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot);
+    return __builtin_amdgcn_make_buffer_rsrc(c.rec + (size_t)slot * kRecBytes, 0, kRecBytes, 0x00020000);
+}
+
+// this lane's probe of its own slot: the key as four 8-byte agent loads
 __device__ __forceinline__ bool key_is(const EvalCache &c, uint32_t slot, const uttt_state_t &s) {
-    const uint32_t *k = reinterpret_cast<const uint32_t *>(c.key + slot);
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(&s);
+    const uint64_t *k = reinterpret_cast<const uint64_t *>(c.rec + (size_t)slot * kRecBytes + kRecKey);
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(&s);
     bool same = true;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) same &= ld_agent(k + i) == w[i];
+    for (int i = 0; i < 4; ++i) same &= ld_agent(k + i) == w[i];
     return same;
 }
 
 // Wave-uniform lookup, the kProbe slots probed by lanes 0..kProbe-1 at once:
 // a hit counts only if no empty slot precedes it in probe order. On a hit the
-// 82 values are copied to dst (LDS) and true is returned.
+// 82 values are copied to dst (LDS, 16-byte aligned, >= 84 floats) and true is returned.
 __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *dst) {
     if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
@@ -261,43 +297,42 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
     const uint32_t slot = (h + (uint32_t)lane) & c.mask;
     uint32_t f = 0u;
     bool same = false;
-    if (lane < kProbe) {  // flag and key in one round trip (the key only counts when the flag is 2)
+    if (lane < kProbe) {  // flag and key in one round trip (the key only counts when the flag is ready)
         f = ld_agent(c.flag + slot);
         same = key_is(c, slot, s);
     }
-    const uint64_t hit = __ballot(lane < kProbe && f == 2u && same);
+    const uint64_t hit = __ballot(lane < kProbe && flag_ready(f) && same);
     const uint64_t empty = __ballot(lane < kProbe && f == 0u);
     if (!hit) return false;
     const int hl = __builtin_ctzll(hit);
     if (empty && __builtin_ctzll(empty) < hl) return false;
     const uint32_t hs = (h + (uint32_t)hl) & c.mask;
-    const float *src = c.val + (size_t)hs * kCacheVal;
-    const float v0 = ld_agent(src + lane);
-    const float v1 = lane < kCacheVal - 64 ? ld_agent(src + 64 + lane) : 0.0f;
-    // seqlock read side: the payload loads must be served before the re-check below is
-    // issued, or the re-check could see the old flag and key while the payload loads see a
-    // replacement in progress (cache_insert: CAS 2 -> 1, rewrite, republish)
+    const uint32_t f1 = (uint32_t)__builtin_amdgcn_readlane((int)f, hl);
+    const rsrc_t r = rec_rsrc(c, hs);
+    floatx4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (lane < kRecLanes - 2) v = __builtin_bit_cast(floatx4_t, __builtin_amdgcn_raw_buffer_load_b128(r, kRecVal + 16 * lane, 0, kSc1));
+    // seqlock read side: the payload loads are served before the re-check is issued; any writer
+    // that touched the record since the probe bumped the flag first (claim), so the re-check differs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bool ok = true;
-    if (lane == 0) ok = ld_agent(c.flag + hs) == 2u && key_is(c, hs, s);
+    if (lane == 0) ok = ld_agent(c.flag + hs) == f1;
     if (!__shfl(ok, 0)) return false;
-    dst[lane] = v0;
-    if (lane < kCacheVal - 64) dst[64 + lane] = v1;
+    if (lane < kRecLanes - 2) *reinterpret_cast<floatx4_t *>(dst + 4 * lane) = v;
     return true;
 }
 
-// Wave-level insert of (s -> pol[0..80], v). Lane 0 claims a slot by CAS; the
-// payload is stored at agent scope and drained (s_waitcnt vmcnt(0)) before the
-// flag is published, so a reader on any XCD that sees the flag sees the data.
-// A concurrent insert of the same key may leave a harmless duplicate. When all
-// kProbe slots hold other positions, one of them (chosen by the hash) is replaced:
-// claimed 2 -> 1 by CAS, rewritten, republished; a reader copying it meanwhile
-// fails its flag-and-key re-check. Entries are exact, so the table never needs
-// clearing while the evaluator is unchanged: it stays warm across moves.
-__device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const float *pol, float v) {
+// Wave-level insert of (s -> 81 priors, value): lane l holds prior l in p0 and prior 64 + l in p1
+// (l < 17). Lane 0 claims a slot by CAS (flag -> odd); the record is stored as 23 16-byte sc1
+// pieces and drained (s_waitcnt vmcnt(0)) before the new version is published, so a reader on
+// any XCD that sees the flag sees the data. A concurrent insert of the same key may leave a
+// harmless duplicate. When all kProbe slots hold other positions, one of them (chosen by the
+// hash) is replaced. Entries are exact, so the table never needs clearing while the evaluator
+// is unchanged: it stays warm across moves.
+__device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v) {
     if (!c.flag) return;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
+    uint32_t pub = 2u;
     // the kProbe slots' flags and keys in one round trip (lanes 0..kProbe-1), then lane 0 acts on
     // the first slot that holds this position or is empty; a lost claim falls back to probing
     // one slot after another from there
@@ -309,7 +344,7 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
         f = ld_agent(c.flag + sl);
         same = key_is(c, sl, s);
     }
-    const uint64_t here = __ballot(lane < kProbe && f == 2u && same);
+    const uint64_t here = __ballot(lane < kProbe && flag_ready(f) && same);
     const uint64_t free_ = __ballot(lane < kProbe && f == 0u);
     const uint64_t either = here | free_;
     const int first = either ? __builtin_ctzll(either) : kProbe;
@@ -324,7 +359,7 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
         for (int i = i0; slot < 0 && !present && i < kProbe; ++i) {
             const uint32_t sl = (h + (uint32_t)i) & c.mask;
             const uint32_t f = ld_agent(c.flag + sl);
-            if (f == 2u && key_is(c, sl, s)) {
+            if (flag_ready(f) && key_is(c, sl, s)) {
                 present = true;
                 break;
             }
@@ -333,24 +368,40 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, const fl
                 break;
             }
         }
-        if (slot < 0 && !present) {  // every probe slot taken: replace one
+        if (slot < 0 && !present) {  // every probe slot taken: replace one (version f -> f + 1 -> f + 2)
             const uint32_t sl = (h + (h >> 29)) & c.mask;
-            if (atomicCAS(c.flag + sl, 2u, 1u) == 2u) {
+            const uint32_t f = ld_agent(c.flag + sl);
+            if (flag_ready(f) && atomicCAS(c.flag + sl, f, f + 1u) == f) {
                 slot = (int)sl;
+                pub = flag_next(f);
                 atomicAdd(stripe_of(c.ctr + 3 * kRow), 1ull);
             }
         }
     }
     slot = __shfl(slot, 0);
     if (slot < 0) return;
-    float *dst = c.val + (size_t)slot * kCacheVal;
-    st_agent(dst + lane, pol[lane]);
-    if (lane < 17) st_agent(dst + 64 + lane, pol[64 + lane]);
-    if (lane == 17) st_agent(dst + 81, v);
-    if (lane < 8) st_agent(reinterpret_cast<uint32_t *>(c.key + slot) + lane, reinterpret_cast<const uint32_t *>(&s)[lane]);
+    pub = (uint32_t)__builtin_amdgcn_readfirstlane((int)pub);
+    // piece j of the record: j < 2 the key's words 4j..4j+3, else values 4(j-2)..4(j-2)+3
+    // (value e < 64: lane e's p0; e < 81: lane e-64's p1; e == 81: v)
+    floatx4_t piece;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = 4 * (lane - 2) + i;
+        const float a = __shfl(p0, e & 63);
+        const float b = __shfl(p1, (e - 64) & 63);
+        piece[i] = e < 64 ? a : (e < 81 ? b : (e == 81 ? v : 0.0f));
+    }
+    const uint32_t *kw = reinterpret_cast<const uint32_t *>(&s);
+    if (lane < 2) {
+        const int o = 4 * lane;
+        piece = floatx4_t{__uint_as_float(kw[o]), __uint_as_float(kw[o + 1]), __uint_as_float(kw[o + 2]),
+                          __uint_as_float(kw[o + 3])};
+    }
+    const rsrc_t r = rec_rsrc(c, (uint32_t)slot);
+    if (lane < kRecLanes) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, piece), r, 16 * lane, 0, kSc1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
-        st_agent(c.flag + slot, 2u);
+        st_agent(c.flag + slot, pub);
         atomicAdd(stripe_of(c.ctr + 2 * kRow), 1ull);
     }
 }
@@ -543,7 +594,7 @@ constexpr int kScanGroup = 4;  // child-scan iterations (64 children each) whose
 template <bool PY>
 __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalCache cache,
                                                    unsigned long long *stats) {
-    __shared__ float s_hit[kWavesPerBlock][kCacheVal];  // a cache hit's values, per wave
+    __shared__ __attribute__((aligned(16))) float s_hit[kWavesPerBlock][84];  // a cache hit's values, per wave
     const int lane = lane_id();
     const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     if (t >= tr.n_trees) return;
@@ -903,8 +954,27 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
     int L = 0;
     const int nodes_before = ctl.node_count;
     if (!per_copy) {
-        const float *pol = policy + (int64_t)slot * pld;
         const float v = rawv;
+        // SURVEY §5 failure detection: a NaN / Inf legal prior or value (uttt_mcts.cpp:144-166 would
+        // expand and back it up silently) stops the tree with kErrNonFinite, which the host raises at
+        // the move boundary (UTTT_ERR_NONFINITE); nothing of it is expanded or cached. A non-finite
+        // entry of an illegal action is never read by the search (it is expanded as the reference
+        // would), but such a row is not cached either: the table only ever holds finite rows.
+        const bool fin0 = __builtin_isfinite(raw0), fin1 = __builtin_isfinite(raw1);
+        {
+            uint32_t m[3];
+            legal_mask(s, m);
+            const bool bad = (bit_of(m, lane) && !fin0) || (lane < 17 && bit_of(m, 64 + lane) && !fin1) ||
+                             !__builtin_isfinite(v);
+            if (__ballot(bad)) {
+                if (lane == 0) {
+                    ctl.status |= kErrNonFinite;
+                    tr.ctl[t] = ctl;
+                }
+                return;
+            }
+        }
+        const bool cacheable = __ballot(!fin0 || (lane < 17 && !fin1)) == 0ull;
         if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f, v,
                            ctl.node_count, tr.py != 0)) {
             if (lane == 0) {
@@ -913,7 +983,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             }
             return;
         }
-        cache_insert(cache, s, pol, v);
+        if (cacheable) cache_insert(cache, s, raw0, raw1, v);
         L = (ctl.node_count - nodes_before) / k;
     } else {
         // the reference's exact call pattern: k results, one per queued copy, applied in order
@@ -929,6 +999,20 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
         if ((int64_t)nb + (int64_t)k * L > pool.cap || L == 0) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
+                tr.ctl[t] = ctl;
+            }
+            return;
+        }
+        bool bad = false;  // any copy's legal prior or value non-finite: nothing is applied (as above)
+        for (int j = 0; j < k; ++j) {
+            const int64_t row = (int64_t)rowbase[slot] + j;
+            const float *pol = policy + row * pld;
+            bad |= (l0 && !__builtin_isfinite(pol[lane])) || (l1 && !__builtin_isfinite(pol[64 + lane])) ||
+                   !__builtin_isfinite(value[row * vld]);
+        }
+        if (__ballot(bad)) {
+            if (lane == 0) {
+                ctl.status |= kErrNonFinite;
                 tr.ctl[t] = ctl;
             }
             return;
@@ -1209,13 +1293,24 @@ __device__ double np_sum(const double *a, int n, int stride) {
     return res;  // n <= 81 < 128: a single pairwise block
 }
 
+// The asynchronous move end's failure check: the first failed tree (lowest slot) and its status
+// into *err (~0 = none), read by the move-end kernels behind it on the stream and by the host.
+__global__ __launch_bounds__(256) void k_tree_err(const TreeCtl *__restrict__ ctl, int n, unsigned long long *err) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t st = (uint32_t)ctl[s].status;
+    if (st & kErrMask) atomicMin(err, ((unsigned long long)s << 32) | st);
+}
+
 // One thread per slot: the per-move tail of self_play_cpp.play (:63-92). The slot's f64
 // policy-target row is worked on in LDS (one column of 81 doubles per thread, conflict-free:
 // the threads of a wave read one row), then stored to this ply's row in HBM once; worked on in
 // HBM, every read after a store was a dependent round trip.
-__global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const TreeCtl *__restrict__ ctl,
-                                                  unsigned long long *err) {
+__global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const unsigned long long *err) {
     __shared__ double s_pt[81][64];
+    // asynchronous form: k_tree_err has folded the failed trees into *err; on a failure this move's
+    // end changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
+    if (err && *err != ~0ull) return;
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     // np.random.choice's random_sample (numpy legacy: two 32-bit draws, 53-bit double), drawn first by
     // every live slot with the whole wave present: a key that runs out is twisted by all 64 lanes
@@ -1247,10 +1342,6 @@ __global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const T
     if (draws) sp.mt_pos[s] = pos;
     const double u = ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
     if (!in) return;
-    if (err) {  // the asynchronous move end reports a failed tree through this word
-        const uint32_t st = ctl[s].status;
-        if (st & kErrMask) atomicMin(err, ((unsigned long long)s << 32) | st);
-    }
     Slot sl = sp.slot[s];
     sl.finished = 0;
     if (!sl.live) {
@@ -1341,8 +1432,9 @@ __global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const T
 
 // One block: give finished games arena rows (slot order) and free slots the
 // next game ids (slot order) — deterministic for a given slot count.
-__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
+__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned long long *err) {
     __shared__ unsigned long long wsum[16];
+    if (err && *err != ~0ull) return;  // a failed tree: the move is not ended (k_move_end)
     const int tid = threadIdx.x;
     const int per = (sp.slots + 1023) / 1024;
     const int b = tid * per, e = min(b + per, sp.slots);
@@ -1415,7 +1507,8 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp) {
 
 // Copy each just-finished game's plies to its arena rows, with values
 // (self_play_cpp.py:95-99: ply 0 gets the final value, then alternating).
-__global__ void k_archive(SelfPlay sp) {
+__global__ void k_archive(SelfPlay sp, const unsigned long long *err) {
+    if (err && *err != ~0ull) return;
     const int s = blockIdx.x;
     const Slot &sl = sp.slot[s];
     if (!sl.finished || sl.fin_offset < 0) return;
@@ -1705,8 +1798,7 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     if (e->d_rowbase) (void)hipFree(e->d_rowbase);
     if (e->cache_owner) {
         if (e->cache.flag) (void)hipFree(e->cache.flag);
-        if (e->cache.key) (void)hipFree(e->cache.key);
-        if (e->cache.val) (void)hipFree(e->cache.val);
+        if (e->cache.rec) (void)hipFree(e->cache.rec);
     }
     if (e->h_count) (void)hipHostFree(e->h_count);
     if (e->h_move) (void)hipHostFree(e->h_move);
@@ -1968,11 +2060,8 @@ static int check_tree_errors(uttt_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     for (int t = 0; t < e->tr.n_trees; ++t) {
         if (ctl[t].status & kErrMask) {
-            set_error("tree %d failed (status 0x%x: %s)", t, ctl[t].status,
-                      (ctl[t].status & kErrCapacity) ? "node pool exhausted"
-                      : (ctl[t].status & kErrDepth)  ? "path deeper than 128"
-                                                     : "no selectable child (NaN statistics)");
-            return (ctl[t].status & kErrSelect) ? UTTT_ERR_ARG : UTTT_ERR_CAPACITY;
+            set_error("tree %d failed (status 0x%x: %s)", t, ctl[t].status, tree_error_text((uint32_t)ctl[t].status));
+            return tree_error_code((uint32_t)ctl[t].status);
         }
     }
     return UTTT_OK;
@@ -2059,7 +2148,7 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipMemsetAsync(sp.slot, 0, sizeof(Slot) * slots, e->stream));
     int64_t ctr[4] = {game_begin, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const unsigned long long *)nullptr);
     if ((rc = check_launch())) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_move, sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2117,10 +2206,10 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
     const int slots = e->sp.slots;
     {
         TimedLaunch tl(e, kKMoveEnd);
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp,
-                           (const TreeCtl *)nullptr, (unsigned long long *)nullptr);
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
-        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
+        const unsigned long long *no_err = nullptr;
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp, no_err);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, no_err);
+        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, no_err);
     }
     if ((rc = check_launch())) return rc;
     int64_t ctr[4];
@@ -2179,10 +2268,14 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
     HIP_TRY(hipMemsetAsync(e->d_err, 0xFF, sizeof(unsigned long long), e->stream));
     {
         TimedLaunch tl(e, kKMoveEnd);
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp,
-                           (const TreeCtl *)e->tr.ctl, e->d_err);
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp);
-        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp);
+        // a failed tree leaves the whole move unended (k_tree_err -> *d_err; the kernels behind it
+        // check it), so the engine is in the state the blocking move end refuses in
+        hipLaunchKernelGGL(k_tree_err, dim3((slots + 255) / 256), dim3(256), 0, e->stream, (const TreeCtl *)e->tr.ctl,
+                           slots, e->d_err);
+        const unsigned long long *err = e->d_err;
+        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp, err);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, err);
+        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, err);
     }
     int rc = check_launch();
     if (rc) return rc;
@@ -2197,11 +2290,8 @@ int uttt_selfplay_move_result(uttt_engine_t *e, int64_t *n_finished, int32_t *n_
     const unsigned long long err = (unsigned long long)e->h_move[4];
     if (err != ~0ull) {
         const uint32_t st = (uint32_t)err, t = (uint32_t)(err >> 32);
-        set_error("tree %u failed (status 0x%x: %s)", t, st,
-                  (st & kErrCapacity) ? "node pool exhausted"
-                  : (st & kErrDepth)  ? "path deeper than 128"
-                                      : "no selectable child (NaN statistics)");
-        return (st & kErrSelect) ? UTTT_ERR_ARG : UTTT_ERR_CAPACITY;
+        set_error("tree %u failed (status 0x%x: %s)", t, st, tree_error_text(st));
+        return tree_error_code(st);
     }
     if (e->h_move[2] > e->sp.arena_cap) {
         set_error("self-play record arena full (%lld plies > %lld)", (long long)e->h_move[2],
@@ -2293,10 +2383,8 @@ int uttt_engine_set_cache(uttt_engine_t *e, int32_t log2_capacity, int32_t clear
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->cache.flag && e->cache_owner) {
         (void)hipFree(e->cache.flag);
-        (void)hipFree(e->cache.key);
-        (void)hipFree(e->cache.val);
-        e->bytes -= (int64_t)((sizeof(uint32_t) + sizeof(uttt_state_t) + sizeof(float) * kCacheVal)
-                              << e->cache_log2);
+        (void)hipFree(e->cache.rec);
+        e->bytes -= (int64_t)((sizeof(uint32_t) + kRecBytes) << e->cache_log2);
     }
     e->cache = EvalCache{};
     e->cache_owner = true;
@@ -2305,9 +2393,8 @@ int uttt_engine_set_cache(uttt_engine_t *e, int32_t log2_capacity, int32_t clear
     if (log2_capacity == 0) return UTTT_OK;
     const size_t cap = (size_t)1 << log2_capacity;
     HIP_TRY(hipMalloc((void **)&e->cache.flag, sizeof(uint32_t) * cap));
-    HIP_TRY(hipMalloc((void **)&e->cache.key, sizeof(uttt_state_t) * cap));
-    HIP_TRY(hipMalloc((void **)&e->cache.val, sizeof(float) * kCacheVal * cap));
-    e->bytes += (int64_t)((sizeof(uint32_t) + sizeof(uttt_state_t) + sizeof(float) * kCacheVal) * cap);
+    HIP_TRY(hipMalloc((void **)&e->cache.rec, (size_t)kRecBytes * cap));
+    e->bytes += (int64_t)((sizeof(uint32_t) + kRecBytes) * cap);
     e->cache.mask = (uint32_t)(cap - 1);
     e->cache.ctr = e->d_cache_ctr;
     return uttt_engine_cache_clear(e);

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("UTTT_ENGINE_LIB") or os.path.join(PKG_ROOT, "libuttt_
 
 UTTT_OK = 0
 ERRORS = {-1: "UTTT_ERR_ARG", -2: "UTTT_ERR_HIP", -3: "UTTT_ERR_CAPACITY", -4: "UTTT_ERR_ORDER",
-          -5: "UTTT_ERR_NODEVICE"}
+          -5: "UTTT_ERR_NODEVICE", -6: "UTTT_ERR_NONFINITE"}
 
 KERNELS = {"select": 0, "apply": 1, "encode": 2, "scan": 3, "move_end": 4, "hash_eval": 5,
            # select latency counters (their value is in "bytes"; no launches)

@@ -74,52 +74,102 @@ def _template():
     return _TPL
 
 
-def history_parts(x, policy, value):
-    """x (n,9,9,3) f32, policy (n,81) f64, value (n,) ints -> the pickle stream of
-    [[x[i], policy[i], int(value[i])] for i in range(n)] as a list of byte buffers."""
-    x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1, 243)
-    policy = np.ascontiguousarray(policy, dtype=np.float64).reshape(-1, 81)
-    value = np.asarray(value, dtype=np.int64).reshape(-1)
-    n = len(x)
-    if n == 0:
-        return [pickle.dumps([], protocol=4)]
-    t = _template()
-    # first ply: the standard pickler's bytes (it defines the memo entries later plies refer to),
-    # with its value re-encoded the way pickle encodes that int
+CHUNK_PLIES = 1 << 16  # plies per body buffer: peak host memory ~ 1.7 KB x this, whatever the file's size
+
+
+def _ply0(t, x0, p0, v0):
+    """The first ply: the standard pickler's bytes (they define the memo entries later plies refer to),
+    its payloads replaced and its value re-encoded the way pickle encodes that int."""
     ply0 = bytearray(t["ply0"])
-    ply0[t["ply0_x"]:t["ply0_x"] + 972] = x[0].tobytes()
-    ply0[t["ply0_p"]:t["ply0_p"] + 648] = policy[0].tobytes()
+    ply0[t["ply0_x"]:t["ply0_x"] + 972] = x0.tobytes()
+    ply0[t["ply0_p"]:t["ply0_p"] + 648] = p0.tobytes()
     vpos = t["ply0_p"] + 648
     tail = bytes(ply0[vpos:])
     # after the payload: BINBYTES trailer ops up to the value opcode 'K\x07' (7 as written above)
     k = tail.rfind(b"K\x07")
-    v0 = pickle.dumps(int(value[0]), protocol=4)[2:-1]  # e.g. K\x00 or J\xff\xff\xff\xff (FRAME-free for ints)
-    ply0 = bytes(ply0[:vpos]) + tail[:k] + v0 + tail[k + 2:]
-    L = len(t["tpl"])
-    body = np.empty((n - 1, L), np.uint8)
+    enc = pickle.dumps(int(v0), protocol=4)[2:-1]  # e.g. K\x00 or J\xff\xff\xff\xff (FRAME-free for ints)
+    return bytes(ply0[:vpos]) + tail[:k] + enc + tail[k + 2:]
+
+
+def _body(t, x, policy, value):
+    """Later plies (x (m,243) f32, policy (m,81) f64, value (m,) ints) as one uint8 buffer."""
+    m = len(x)
+    body = np.empty((m, len(t["tpl"])), np.uint8)
     body[:] = t["tpl"]
-    body[:, t["ox"]:t["ox"] + 972] = x[1:].view(np.uint8).reshape(n - 1, 972)
-    body[:, t["op"]:t["op"] + 648] = policy[1:].view(np.uint8).reshape(n - 1, 648)
-    body[:, t["ov"]:t["ov"] + 4] = value[1:].astype("<i4").view(np.uint8).reshape(n - 1, 4)
-    return [t["head"], ply0, memoryview(body.reshape(-1)), b"e."]
+    body[:, t["ox"]:t["ox"] + 972] = x.view(np.uint8).reshape(m, 972)
+    body[:, t["op"]:t["op"] + 648] = policy.view(np.uint8).reshape(m, 648)
+    body[:, t["ov"]:t["ov"] + 4] = np.asarray(value).astype("<i4").view(np.uint8).reshape(m, 4)
+    return memoryview(body.reshape(-1))
+
+
+def _norm(x, policy, value):
+    return (np.ascontiguousarray(x, dtype=np.float32).reshape(-1, 243),
+            np.ascontiguousarray(policy, dtype=np.float64).reshape(-1, 81),
+            np.asarray(value, dtype=np.int64).reshape(-1))
+
+
+def stream_parts(chunks):
+    """chunks: an iterable of (x, policy, value) ply blocks, in file order -> the pickle stream of
+    their concatenated plies as byte buffers, one body buffer per block (so a caller that feeds
+    bounded blocks holds one block's bytes at a time)."""
+    t = None
+    for x, p, v in chunks:
+        x, p, v = _norm(x, p, v)
+        if not len(x):
+            continue
+        if t is None:
+            t = _template()
+            yield t["head"]
+            yield _ply0(t, x[0], p[0], v[0])
+            x, p, v = x[1:], p[1:], v[1:]
+            if not len(x):
+                continue
+        yield _body(t, x, p, v)
+    if t is None:
+        yield pickle.dumps([], protocol=4)
+    else:
+        yield b"e."
+
+
+def history_parts(x, policy, value):
+    """x (n,9,9,3) f32, policy (n,81) f64, value (n,) ints -> the pickle stream of
+    [[x[i], policy[i], int(value[i])] for i in range(n)] as a list of byte buffers."""
+    x, policy, value = _norm(x, policy, value)
+    return list(stream_parts((x[i:i + CHUNK_PLIES], policy[i:i + CHUNK_PLIES], value[i:i + CHUNK_PLIES])
+                             for i in range(0, max(len(x), 1), CHUNK_PLIES)))
 
 
 def history_bytes(x, policy, value):
     return b"".join(bytes(b) for b in history_parts(x, policy, value))
 
 
+def _record_chunks(records, cap=None):
+    """Per-game records -> ply blocks of about cap plies (whole games), each concatenated on its own."""
+    cap = CHUNK_PLIES if cap is None else cap
+    buf, n = [], 0
+    for r in records:
+        buf.append(r)
+        n += len(r["values"])
+        if n >= cap:
+            yield _cat(buf)
+            buf, n = [], 0
+    if buf:
+        yield _cat(buf)
+
+
+def _cat(recs):
+    return (np.concatenate([r["inputs"].reshape(-1, 243) for r in recs]),
+            np.concatenate([r["policies"] for r in recs]),
+            np.concatenate([r["values"] for r in recs]))
+
+
 def write_history_file(records, path):
     """records (games sorted by id, each with inputs/policies/values, as SelfPlay.records or the
-    gathered records) -> the .history file at path. Returns the byte count."""
-    if records:
-        x = np.concatenate([r["inputs"].reshape(-1, 243) for r in records])
-        p = np.concatenate([r["policies"] for r in records])
-        v = np.concatenate([r["values"] for r in records])
-    else:
-        x, p, v = np.zeros((0, 243), np.float32), np.zeros((0, 81)), np.zeros(0, np.int64)
+    gathered records) -> the .history file at path, streamed in blocks of about CHUNK_PLIES plies
+    (host memory beyond the records themselves stays ~110 MB at any file size). Returns the byte count."""
     nbytes = 0
     with open(path, "wb") as f:
-        for part in history_parts(x, p, v):
+        for part in stream_parts(_record_chunks(records)):
             f.write(part)
             nbytes += len(part)
     return nbytes
@@ -145,4 +195,4 @@ def lists_equal(la, lb):
     return True
 
 
-__all__ = ["files_equal", "history_bytes", "history_parts", "lists_equal", "write_history_file"]
+__all__ = ["files_equal", "history_bytes", "history_parts", "lists_equal", "stream_parts", "write_history_file"]

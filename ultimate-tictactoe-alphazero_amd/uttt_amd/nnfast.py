@@ -114,6 +114,10 @@ class FusedNetworkEvaluator:
         if engine is not None:
             dev = torch.device("cuda", engine.device)
             self.max_batch = max_batch or engine.max_trees
+            if self.max_batch < engine.max_trees:
+                # the stem writes one row per pending leaf (up to every tree of the engine; in
+                # device-count rounds its grid covers them all) and k_apply reads as many rows
+                raise ValueError(f"max_batch {self.max_batch} < the engine's {engine.max_trees} trees")
         else:
             dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
             if max_batch is None:
