@@ -15,7 +15,7 @@ from uttt_amd.model import fold_bn, random_network  # noqa: E402
 from uttt_amd.nnfast import amax, wino3h_weights, _p  # noqa: E402
 
 lib = _lib.load()
-    dlib = _lib.load_diag()
+dlib = _lib.load_diag()
 dlib.uttt_diag_wino3h_ablation.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_float] + [ctypes.c_void_p] * 3 + \
     [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
 net = random_network(0)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU session. STEPS (default "tests smoke train cycle bench") picks the steps, in this order:
+# Round-4 GPU session. quick: headline + tree-only short bench lines. STEPS (default "tests smoke train cycle bench") picks the steps, in this order:
 #   tests  every -m gpu test (verbose, per-test timeout)     smoke  __graft_entry__.smoke()
 #   train  tools/bench_train.py (eager / HIP graph / graph + channels-last)
 #   cycle  tools/bench_cycle.py (BASELINE configs[4] on one GPU)
@@ -34,6 +34,8 @@ for s in $STEPS; do
     tprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tprof -o train \
                -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \
                > $OUT/tprof.log 2>&1 ;;
+    selcyc) timeout -k 10 300 python -u tools/diag/select_cycles.py ${SELCYC_ARGS:-} > $OUT/select_cycles.log 2>&1 ;;
+    stamps) timeout -k 10 300 python -u tools/diag/wino3h_stamps.py 1344 16384 > $OUT/stamps.log 2>&1 ;;
     lat)   timeout -k 10 300 python -u tools/diag/latency_single.py > $OUT/latency.log 2>&1 ;;
     vsmall) VARIANTS= timeout -k 10 300 python -u tools/diag/wino3h_variants.py 250 500 1000 > $OUT/variants_small.log 2>&1 ;;
     tcomp) timeout -k 10 600 python -u tools/diag/train_compare.py > $OUT/train_compare.log 2>&1 ;;
@@ -68,6 +70,11 @@ for s in $STEPS; do
     chase) # dependent-load latency (k_select's latency-model unit); the bench reads profiles/r*/chase.json
            timeout -k 10 180 tools/diag/chase 200 > $OUT/chase.json && cp $OUT/chase.json profiles/r4/chase.json ;;
     bench) timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 ;;
+    quick) # headline and tree-only, short runs (no variants / CPU baselines / isolated conv)
+           timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps 10 --warmup 4 \
+             > $OUT/quick_head.log 2>&1 && \
+           timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps 10 --warmup 4 \
+             --evaluator hash --lanes 1 --age 100 > $OUT/quick_tree.log 2>&1 ;;
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/prof_bench.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -179,27 +179,36 @@ __device__ __forceinline__ void wave_argmax(float &v, int &i) {
     }
 }
 
-// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction):
-// within each row of 16 lanes (quad swaps, half-row and row mirrors), then row 0 into row 1
-// and row 2 into row 3 (row_bcast15), then row 1 into rows 2-3 (row_bcast31). The order
-// (larger value, then smaller index) is total, so any reduction tree gives the same winner;
-// the result is valid in lane 63.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void argmax_dpp(float &v, int &i) {
-    const int vb = __float_as_int(v);
-    const float ov = __int_as_float(__builtin_amdgcn_update_dpp(vb, vb, CTRL, ROWS, 0xF, false));
-    const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, ROWS, 0xF, false);
-    const bool take = ov > v || (ov == v && oi < i);
-    v = take ? ov : v;
-    i = take ? oi : i;
+// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction), on one
+// 64-bit key per lane: the value's bits mapped to an order-preserving unsigned (-0 canonicalised to
+// +0, which compares equal to it; values are never NaN here: the per-lane scan's strict '>' from
+// -1e9 never takes one) above the complemented index, so "larger value, then smaller index" is the
+// unsigned order of the keys and each step is one compare and two selects, no branches. The order
+// is total, so any reduction tree gives the same winner: within each row of 16 lanes (quad swaps,
+// half-row and row mirrors), then row 0 into row 1 and row 2 into row 3 (row_bcast15), then row 1
+// into rows 2-3 (row_bcast31). The winner's index is valid in lane 63.
+__device__ __forceinline__ uint64_t argmax_key(float v, int i) {
+    uint32_t b = __float_as_uint(v + 0.0f);
+    b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    return ((uint64_t)b << 32) | (uint64_t)(~(uint32_t)i);
 }
-__device__ __forceinline__ void wave_argmax_to63(float &v, int &i) {
-    argmax_dpp<0xB1, 0xF>(v, i);   // quad_perm [1,0,3,2]
-    argmax_dpp<0x4E, 0xF>(v, i);   // quad_perm [2,3,0,1]
-    argmax_dpp<0x141, 0xF>(v, i);  // row_half_mirror
-    argmax_dpp<0x140, 0xF>(v, i);  // row_mirror
-    argmax_dpp<0x142, 0xA>(v, i);  // row_bcast15 -> rows 1, 3
-    argmax_dpp<0x143, 0xC>(v, i);  // row_bcast31 -> rows 2, 3
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void argmax_dpp(uint64_t &k) {
+    const int lo = (int)(uint32_t)k, hi = (int)(uint32_t)(k >> 32);
+    const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWS, 0xF, false);
+    const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWS, 0xF, false);
+    const uint64_t o = ((uint64_t)ohi << 32) | olo;
+    k = o > k ? o : k;
+}
+__device__ __forceinline__ int wave_argmax_to63(float v, int i) {
+    uint64_t k = argmax_key(v, i);
+    argmax_dpp<0xB1, 0xF>(k);   // quad_perm [1,0,3,2]
+    argmax_dpp<0x4E, 0xF>(k);   // quad_perm [2,3,0,1]
+    argmax_dpp<0x141, 0xF>(k);  // row_half_mirror
+    argmax_dpp<0x140, 0xF>(k);  // row_mirror
+    argmax_dpp<0x142, 0xA>(k);  // row_bcast15 -> rows 1, 3
+    argmax_dpp<0x143, 0xC>(k);  // row_bcast31 -> rows 2, 3
+    return (int)~(uint32_t)k;
 }
 
 __device__ __forceinline__ float readlane_f(float v, int l) {
@@ -445,9 +454,36 @@ __device__ float np_sum_f32_legal(float p0, float p1, uint64_t b0, uint64_t b1, 
 }
 
 // raw0 / raw1: this lane's prior of action lane / 64 + lane (lane < 17), loaded by the caller
+// The sequential f32 sum of the legal priors in action order (uttt_mcts.cpp:150-153): each legal
+// prior is stored at its rank in the wave's LDS row (zeros pad the row to a multiple of 4; adding
+// +0.0 to a sum that started at +0.0 changes nothing), then every lane reads the row back by
+// broadcast 16-byte reads and adds it up in order: one dependent add per prior, instead of a scalar
+// find-first-bit, a v_readlane and an add per prior.
+__device__ __forceinline__ float seq_sum_legal(float *row /* LDS, 16-B aligned, >= 84 floats */, float p0, float p1,
+                                               bool l0, bool l1, int i0, int i1, int L) {
+    const int lane = lane_id();
+    if (l0) row[i0] = p0;
+    if (l1) row[i1] = p1;
+    const int L4 = (L + 3) & ~3;
+    if (lane >= L && lane < L4) row[lane] = 0.0f;  // L4 - L < 4 <= 64: lanes L .. L4-1 pad
+    // the other lanes' stores before any lane's reads (LDS executes a wave's accesses in order; the
+    // wait and the clobber keep the compiler from hoisting the reads above the stores)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float sum = 0.0f;
+    const float4 *r4 = reinterpret_cast<const float4 *>(row);
+    for (int i = 0; i < L4 / 4; ++i) {
+        const float4 q = r4[i];
+        sum += q.x;
+        sum += q.y;
+        sum += q.z;
+        sum += q.w;
+    }
+    return sum;
+}
+
 __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi, int k,
                               const uttt_state_t &s, float raw0, float raw1, float v, int &node_count,
-                              bool py = false) {
+                              bool py = false, float *row = nullptr) {
     const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
@@ -465,6 +501,8 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     float sum = 0.0f;
     if (py) {
         sum = np_sum_f32_legal(p0, p1, b0, b1, L);
+    } else if (row) {
+        sum = seq_sum_legal(row, p0, p1, l0, l1, i0, i1, L);
     } else {
         for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
         for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
@@ -591,6 +629,112 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 constexpr int kSelectBudget = 8;
 constexpr int kScanGroup = 4;  // child-scan iterations (64 children each) whose loads are issued together
 
+// k_select phase clock. Product build: empty (every call compiles to nothing). Diagnostics engine
+// build (-DUTTT_DIAG_BUILD, libuttt_engine_diag.so, tools/diag/select_cycles.py): each mark drains the
+// wave's memory counters, reads s_memtime and charges the cycles since the previous mark to one phase;
+// at the end lane 0 adds the wave's phases into g_sel_cyc (all trees, and separately the trees with at
+// least kSelHeavyTrips dependent round trips in the launch: the ones that set its length).
+enum SelPhase {
+    kSpRoot = 0,    // the descent's root link and visits (load wait)
+    kSpLoad,        // a child-scan group's loads (wait)
+    kSpPuct,        // PUCT values and the per-lane strict '>' scan
+    kSpArgmax,      // wave arg-max, winner's registers
+    kSpNext,        // next_state, path bookkeeping
+    kSpLeaf,        // is_lose / legal count of the leaf
+    kSpTerminal,    // terminal backup + fence
+    kSpProbe,       // evaluation-cache probe, payload, re-check
+    kSpExpand,      // expand + backup of a cache hit (prior sum, child blocks, path)
+    kSpHitTail,     // fence + counters after a hit
+    kSpQueue,       // pending-leaf record
+    kSpCount
+};
+constexpr int kSelHeavyTrips = 24;
+#ifdef UTTT_DIAG_BUILD
+__device__ unsigned long long g_sel_cyc[2 * kSpCount + 2];  // [all trees][heavy trees], then tree counts
+struct SelClock {
+    unsigned long long t, acc[kSpCount];
+    __device__ __forceinline__ void start() {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        t = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < kSpCount; ++i) acc[i] = 0ull;
+    }
+    template <int P>
+    __device__ __forceinline__ void mark() {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long n = __builtin_amdgcn_s_memtime();
+        acc[P] += n - t;
+        t = n;
+    }
+    __device__ __forceinline__ void flush(unsigned int trips) {
+        if ((threadIdx.x & 63) != 0) return;
+        const int h = trips >= (unsigned int)kSelHeavyTrips;
+#pragma unroll
+        for (int i = 0; i < kSpCount; ++i) {
+            atomicAdd(&g_sel_cyc[i], acc[i]);
+            if (h) atomicAdd(&g_sel_cyc[kSpCount + i], acc[i]);
+        }
+        atomicAdd(&g_sel_cyc[2 * kSpCount], 1ull);
+        if (h) atomicAdd(&g_sel_cyc[2 * kSpCount + 1], 1ull);
+    }
+};
+#else
+struct SelClock {
+    __device__ __forceinline__ void start() {}
+    template <int P>
+    __device__ __forceinline__ void mark() {}
+    __device__ __forceinline__ void flush(unsigned int) {}
+};
+#endif
+
+// One scan group of NJ x 64 children of a node (uttt_mcts.cpp:62-78). Every load of the group is
+// issued before the first compare (one memory round trip per group; a node expanded by a flush of
+// k = 8 copies has up to 8 x 81 children), and each child's link word and visits come with it, so
+// the winner's are read from its lane's registers after the arg-max instead of from memory. The PUCT
+// values of the group are straight-line code: every child's two correctly rounded divisions are
+// independent of every other's, so their latencies overlap instead of running one child after
+// another behind per-child branches. Children past cnt (clamped loads) never win; the compare is the
+// reference's strict '>' in child order.
+template <int NJ>
+__device__ __forceinline__ void puct_group(const int32_t *__restrict__ N, const float *__restrict__ W,
+                                           const float *__restrict__ P, const uint2 *__restrict__ LK, int first,
+                                           int c0, int cnt, float sq, int lane, float &best, int &bi, int &bn,
+                                           uint2 &bl, SelClock &clk) {
+    int cn[NJ];
+    float cw[NJ], cp[NJ];
+    uint2 cl[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = min(c0 + j * kWave + lane, cnt - 1);
+        cn[j] = N[first + c];
+        cw[j] = W[first + c];
+        cp[j] = P[first + c];
+        cl[j] = LK[first + c];
+    }
+    clk.mark<kSpLoad>();
+    float v[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off); the
+        // reference divides only when n > 0, and an unvisited child's quotient here is discarded
+        const float qd = -cw[j] / (float)max(cn[j], 1);
+        const float q = cn[j] > 0 ? qd : 0.0f;
+        const float u = cp[j] * sq / (float)(1 + cn[j]);
+        v[j] = q + u;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = c0 + j * kWave + lane;
+        const bool take = c < cnt && v[j] > best;
+        best = take ? v[j] : best;
+        bi = take ? c : bi;
+        bn = take ? cn[j] : bn;
+        bl.x = take ? cl[j].x : bl.x;
+        bl.y = take ? cl[j].y : bl.y;
+    }
+    clk.mark<kSpPuct>();
+}
+
 template <bool PY>
 __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalCache cache,
                                                    unsigned long long *stats) {
@@ -606,6 +750,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     // one per child-scan group, and for a completion in place the cache probe, payload and re-check,
     // the path's read-modify-write and the fence
     unsigned int trips = 1;
+    SelClock clk;
+    clk.start();
     if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
         const size_t base = (size_t)t * pool.cap;
         int32_t *__restrict__ N = pool.n + base;
@@ -622,6 +768,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             uint2 lk = LK[0];
             int node_n = N[0];  // the current node's visits (below the root: from the parent's scan)
             ++trips;
+            clk.mark<kSpRoot>();
             bool fail = false;
             for (;;) {
                 const int cnt = PY ? meta_L(lk.y) : meta_k(lk.y) * meta_L(lk.y);
@@ -642,45 +789,17 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
                         ++trips;
-                        int cn[kScanGroup];
-                        float cw[kScanGroup], cp[kScanGroup];
-                        uint2 cl[kScanGroup];
-#pragma unroll
-                        for (int j = 0; j < kScanGroup; ++j) {
-                            if (c0 + j * kWave < cnt) {  // wave-uniform
-                                const int c = min(c0 + j * kWave + lane, cnt - 1);
-                                cn[j] = N[first + c];
-                                cw[j] = W[first + c];
-                                cp[j] = P[first + c];
-                                cl[j] = LK[first + c];
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < kScanGroup; ++j) {
-                            if (c0 + j * kWave < cnt) {
-                                const int c = c0 + j * kWave + lane;
-                                // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off);
-                                // the per-lane scan stays strict '>' in child order
-                                const float q = (cn[j] > 0) ? (-cw[j] / (float)cn[j]) : 0.0f;
-                                const float u = cp[j] * sq / (float)(1 + cn[j]);
-                                const float v = q + u;
-                                const bool take = c < cnt && v > best;
-                                best = take ? v : best;
-                                bi = take ? c : bi;
-                                bn = take ? cn[j] : bn;
-                                bl.x = take ? cl[j].x : bl.x;
-                                bl.y = take ? cl[j].y : bl.y;
-                            }
-                        }
+                        if (cnt - c0 <= kWave) puct_group<1>(N, W, P, LK, first, c0, cnt, sq, lane, best, bi, bn, bl, clk);
+                        else puct_group<kScanGroup>(N, W, P, LK, first, c0, cnt, sq, lane, best, bi, bn, bl, clk);
                     }
-                    wave_argmax_to63(best, bi);
-                    bi = __builtin_amdgcn_readlane(bi, 63);
+                    bi = __builtin_amdgcn_readlane(wave_argmax_to63(best, bi), 63);
                     if (bi != kNone) {  // the winner's lane holds its visits and link word
                         const int wl = bi & (kWave - 1);
                         node_n = __builtin_amdgcn_readlane(bn, wl);
                         lk = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)bl.x, wl),
                                         (uint32_t)__builtin_amdgcn_readlane((int)bl.y, wl));
                     }
+                    clk.mark<kSpArgmax>();
                 } else {
                     const int total = N[node] - kself;  // == sum of children's visits
                     trips += 2u + (unsigned int)((cnt + kWave - 1) / kWave);  // N[node], the scan, LK[node]
@@ -733,11 +852,14 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 }
                 if (PY) lk = LK[node];
                 s = next_state(s, meta_action(lk.y));
+                clk.mark<kSpNext>();
             }
             if (fail) break;
             levels += (unsigned int)(depth + 1);
             const bool lose = is_lose(s);
-            if (lose || legal_count(s) == 0u) {
+            const bool no_legal = legal_count(s) == 0u;
+            clk.mark<kSpLeaf>();
+            if (lose || no_legal) {
                 // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
                 // backpropagate adds it at the leaf and flips sign upwards (:47-54).
                 const float v = -(lose ? -1.0f : 0.0f);
@@ -754,6 +876,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 wave_memory_fence();
                 trips += 2;
                 bytes += 16ull * (unsigned long long)(depth + 1);
+                clk.mark<kSpTerminal>();
                 ++sims_done;
                 if (sims_done >= tr.sims) break;
                 if (--budget == 0) {
@@ -767,17 +890,22 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             const int k = min(tr.batch, tr.sims - sims_done);
             float *cv = s_hit[threadIdx.x >> 6];
             trips += cache.flag ? 1 : 0;
-            if (cache_lookup(cache, s, cv)) {  // the flush's evaluation is already known: apply it now
+            const bool hit = cache_lookup(cache, s, cv);
+            clk.mark<kSpProbe>();
+            if (hit) {  // the flush's evaluation is already known: apply it now
                 trips += 4;
-                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, cv[lane], lane < 17 ? cv[64 + lane] : 0.0f,
-                                   cv[81], ctl.node_count,
-                                   PY)) {
+                // cv doubles as the prior sum's row: its values are in registers before the call
+                const float h0 = cv[lane], h1 = lane < 17 ? cv[64 + lane] : 0.0f, hv = cv[81];
+                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, h0, h1, hv, ctl.node_count, PY,
+                                   cv)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
                 }
+                clk.mark<kSpExpand>();
                 wave_memory_fence();
                 if (lane == 0) atomicAdd(stripe_of(cache.ctr), 1ull);
                 bytes += 20ull * (unsigned long long)(k * meta_L(LK[node].y)) + 16ull * (depth + 1);
+                clk.mark<kSpHitTail>();
                 sims_done += k;
                 if (sims_done >= tr.sims) break;
                 if (--budget == 0) {
@@ -801,11 +929,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             }
             // 3: this leaf's k simulations leave the tree more to do (after its apply)
             pend = sims_done + k < tr.sims ? 3 : 1;
+            clk.mark<kSpQueue>();
             break;
         }
         ctl.sims_done = sims_done;
         if (lane == 0) tr.ctl[t] = ctl;
     }
+    clk.flush(trips);
     if (lane == 0) {
         tr.pending[t] = pend;
         if (stats && bytes) atomicAdd(stripe_of(stats + kKSelect * kRow), bytes);
@@ -926,6 +1056,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
                                                   int64_t pld, const float *__restrict__ value, int64_t vld,
                                                   const int32_t *__restrict__ rowbase, int per_copy,
                                                   unsigned long long *bytes_ctr) {
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];  // the prior sum's row, per wave
     const int lane = lane_id();
     const int slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
     // two dependent round trips before the work: the count with this slot's tree (tree_of holds
@@ -976,7 +1107,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
         }
         const bool cacheable = __ballot(!fin0 || (lane < 17 && !fin1)) == 0ull;
         if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f, v,
-                           ctl.node_count, tr.py != 0)) {
+                           ctl.node_count, tr.py != 0, s_row[threadIdx.x >> 6])) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
@@ -2468,6 +2599,18 @@ int uttt_engine_kernel_stats(uttt_engine_t *e, int32_t kernel, double *total_ms,
     if (bytes) *bytes = (int64_t)sum;
     return UTTT_OK;
 }
+
+#ifdef UTTT_DIAG_BUILD
+// Diagnostics engine build only: k_select's phase cycles (SelClock), out[2 * kSpCount + 2]; reset zeroes them.
+int uttt_diag_select_cycles(unsigned long long *out, int32_t reset) {
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_cyc), sizeof(g_sel_cyc)) != hipSuccess) return UTTT_ERR_HIP;
+    if (reset) {
+        static const unsigned long long zero[2 * kSpCount + 2] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_cyc), zero, sizeof(zero)) != hipSuccess) return UTTT_ERR_HIP;
+    }
+    return UTTT_OK;
+}
+#endif
 
 int uttt_engine_reset_stats(uttt_engine_t *e) {
     if (!e) return UTTT_ERR_ARG;
