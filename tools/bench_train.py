@@ -50,7 +50,9 @@ def main():
     for var in args.variants.split(","):
         kw = {"eager": dict(graph=False), "graph": dict(graph=True), "graph_cl": dict(graph=True, channels_last=True),
               "graph_f16": dict(graph=True, precision="f16"),
-              "graph_f16_cl": dict(graph=True, precision="f16", channels_last=True)}[var]
+              "graph_f16_cl": dict(graph=True, precision="f16", channels_last=True),
+              # the per-rank shard of the global batch 128 on 8 data-parallel ranks (DESIGN §7c projection)
+              "graph_b16": dict(graph=True, batch_size=16)}[var]
         model = random_network(0)
         train.train_network(model, h[:1024], epochs=1, device=dev, log=None, **kw)  # warm-up (MIOpen tuning)
         model = random_network(0)
@@ -59,10 +61,38 @@ def main():
         losses = train.train_network(model, h, epochs=args.epochs, device=dev, log=None, **kw)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        nsteps = args.epochs * -(-args.samples // kw.get("batch_size", train.BATCH_SIZE))
         out["variants"][var] = {"value": round(args.epochs * args.samples / dt, 1),
-                                "ms_per_step": round(1e3 * dt / steps, 3),
+                                "ms_per_step": round(1e3 * dt / nsteps, 3),
+                                "batch": kw.get("batch_size", train.BATCH_SIZE),
                                 "s_per_epoch": round(dt / args.epochs, 3), "losses": losses}
         print(var, out["variants"][var], file=sys.stderr, flush=True)
+    if "graph_b16" in out["variants"]:
+        # 8-rank data-parallel projection of the reference's loop (global batch 128 = 8 x 16): per step the
+        # rank's batch-16 graphed step plus the gradient all-reduce (4.77 M f32 = 19.1 MB). The all-reduce is
+        # not measured on one GPU: a ring over 8 ranks moves 2 x 7/8 x 19.1 MB per rank; priced at an
+        # assumed 100 GB/s bus bandwidth per rank (xGMI: 7 links x ~153 GB/s peak, MI355X_MICROARCH.md)
+        # and floored by this GPU's own 19.1 MB device copy (measured)
+        nbytes = 4765338 * 4
+        a = torch.empty(nbytes // 4, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            b.copy_(a)
+        torch.cuda.synchronize()
+        copy_ms = (time.perf_counter() - t0) * 1e3 / 50
+        ring_ms = 2 * 7 / 8 * nbytes / 100e9 * 1e3
+        step16 = out["variants"]["graph_b16"]["ms_per_step"]
+        steps_per_epoch = -(-args.samples // train.BATCH_SIZE)
+        out["dp8_projection"] = {"rank_step_ms_b16": step16, "grad_bytes": nbytes, "device_copy_ms": round(copy_ms, 4),
+                                 "allreduce_ms_assumed": round(max(ring_ms, copy_ms), 4),
+                                 "step_ms": round(step16 + max(ring_ms, copy_ms), 3),
+                                 "s_per_epoch": round(steps_per_epoch * (step16 + max(ring_ms, copy_ms)) / 1e3, 3),
+                                 "samples_per_s": round(args.samples / (steps_per_epoch * (step16 + max(ring_ms, copy_ms)) / 1e3), 1),
+                                 "basis": "8 ranks x batch 16 = the reference's global batch 128; the all-reduce is not "
+                                          "overlapped in this estimate (DDP overlaps it with the backward)"}
     best = max(out["variants"], key=lambda k: out["variants"][k]["value"])
     out["value"] = out["variants"][best]["value"]
     out["best_variant"] = best

@@ -23,9 +23,13 @@ for s in $STEPS; do
     cycle) timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle.json ${CYCLE_ARGS:-} > $OUT/cycle.log 2>&1 ;;
     cycle16) UTTT_TRAIN_PRECISION=f16 timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle_f16.json ${CYCLE_ARGS:-} > $OUT/cycle_f16.log 2>&1 ;;
     hist)  timeout -k 10 300 python -u tools/bench_history.py > $OUT/history.log 2>&1 ;;
-    pmctree) PMC_OUT=gpurun_out/pmc_tree PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
-               > $OUT/pmc_tree.log 2>&1 ;;
-    pmcsel) timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 ;;
+    pmctree) PMC_OUT=$OUT/pmc_tree PMC_AGE=100 PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
+               > $OUT/pmc_tree.log 2>&1 && \
+             python tools/pmc_summary.py $OUT/pmc_tree $OUT/pmc_tree/p1.log $OUT/pmc_select_tree.json k_select >> $OUT/pmc_tree.log && \
+             python tools/pmc_summary.py $OUT/pmc_tree $OUT/pmc_tree/p1.log $OUT/pmc_apply_tree.json k_apply >> $OUT/pmc_tree.log ;;
+    pmcsel) PMC_OUT=$OUT/pmc_sel timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 && \
+             python tools/pmc_summary.py $OUT/pmc_sel $OUT/pmc_sel/p1.log $OUT/pmc_select.json k_select >> $OUT/pmc_select.log && \
+             python tools/pmc_summary.py $OUT/pmc_sel $OUT/pmc_sel/p1.log $OUT/pmc_apply.json k_apply >> $OUT/pmc_select.log ;;
     pmcconv) timeout -k 10 600 bash tools/pmc_conv.sh > $OUT/pmc_conv.log 2>&1 && \
              python tools/pmc_conv_summary.py gpurun_out/pmc_conv ${N:-1344} $OUT/pmc_conv.json >> $OUT/pmc_conv.log 2>&1 ;;
     pmcl2) timeout -k 10 1000 bash tools/pmc_l2.sh > $OUT/pmc_l2.log 2>&1 && \

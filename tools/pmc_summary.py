@@ -37,7 +37,10 @@ def main(d, bench_log, out, kernel="k_select"):
         "traffic_bytes_reads_doubled": (2 * fetch + write) * 1024,
         "algo_bytes_per_launch_bench": roof["algo_bytes_per_launch"],
         "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE, then WRITE_SIZE, then TCC_EA0_RDREQ_sum, "
-                  "separate passes of `bench.py --steps 6 --warmup 2 --age 40`; KiB -> bytes",
+                  "separate passes of `bench.py --steps 6 --warmup 2 --age " + str(bench["config"]["aged_moves"]) +
+                  "`; KiB -> bytes; algorithmic bytes from the first pass's own bench line",
+        "aged_moves": bench["config"]["aged_moves"],
+        "traffic_over_algo": round((fetch + write) * 1024 / max(roof["algo_bytes_per_launch"], 1), 3),
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

@@ -125,9 +125,11 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
         case 5: UTTT_V(kBufferX | kNoALookahead, 5); break;
         case 6: UTTT_V(kNoALookahead, 3); break;
         case 20: UTTT_V(kFoldBuiltin, 3); break;
-        case 70: UTTT_V(kFoldScalarAsm, 3); break;
-        case 71: UTTT_V(kFoldScalarAsm | kBufferX, 3); break;
-        case 72: UTTT_V(kFoldScalarAsm | kBufferX, 4); break;
+        case 70: UTTT_V(kFoldPacked, 3); break;  // the round-3 product (packed fold)
+        case 71: UTTT_V(kBufferX, 3); break;
+        case 72: UTTT_V(kBufferX, 4); break;
+        case 73: UTTT_V(kStagger | kFoldPacked, 3); break;
+        case 74: UTTT_V(kStagger, 3); break;
         case 40: UTTT_V(kALook2, 2); break;
         case 41: UTTT_V(kALook2, 3); break;
         case 42: UTTT_V(kALook2 | kBufferX, 3); break;

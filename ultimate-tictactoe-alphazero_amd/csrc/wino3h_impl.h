@@ -62,8 +62,10 @@ constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS lat
 constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
 constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
-constexpr int kFoldScalarAsm = 1 << 29;   // fold as inline-asm scalar v_add_f32 / v_fma_f32 pairs (packed f32 ops
-                                          // beside MFMAs cost ~4x their issue slot, MI355X_MICROARCH.md)
+constexpr int kStagger = 1 << 30;         // waves 4-7 walk the 25 points from kStaggerRot on (their SIMD partners
+                                          // from 0), so the partners' fold-free and fold-heavy points interleave
+constexpr int kStaggerRot = 12;
+constexpr int kFoldPacked = 1 << 29;      // fold as inline-asm packed v_pk_add_f32 / v_pk_fma_f32 (rounds 1-3)
 
 struct Acc {
     floatx2 p[4];  // pairs 0-1: rows block 0 (4 tiles), 2-3: block 1
@@ -111,7 +113,11 @@ __device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], flo
             if constexpr (K == 1) S[a * 5 + v].p[j] = S[a * 5 + v].p[j] + m[j];
             else if constexpr (K == -1) S[a * 5 + v].p[j] = S[a * 5 + v].p[j] - m[j];
             else S[a * 5 + v].p[j] = __builtin_elementwise_fma(m[j], K == 2 ? k2 : k4, S[a * 5 + v].p[j]);
-        } else if constexpr (MODE & kFoldScalarAsm) {
+        } else if constexpr (!(MODE & kFoldPacked)) {
+            // product: two scalar ops per pair. A packed f32 op beside MFMAs costs several times its
+            // issue slot (MI355X_MICROARCH.md, price of one filler: 2 v_pk_add_f32 +26 cycles against 2
+            // v_fma_f32); the scalar pair gives the same bits (round 4, tools/diag/wino3h_variants.py:
+            // 1,344 boards 71.7-73.3 -> 67.2-67.6 us, 16,384 boards 722-737 -> 689-694 us)
             floatx2 &t = S[a * 5 + v].p[j];
             if constexpr (K == 1) {
                 asm volatile("v_add_f32 %0, %0, %1" : "+v"(t.x) : "v"(m[j].x));
@@ -167,10 +173,13 @@ __device__ __forceinline__ BFrag load_b(rsrc_t u, int xi, int chunk, int voff) {
     b.l = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff + UPLANE, soff, 0));
     return b;
 }
-template <int XI>
+// the XI-th point a wave visits: the points in order from ROT (0 in the product)
+template <int XI, int ROT>
+__host__ __device__ constexpr int pt() { return (XI + ROT) % NP; }
+template <int XI, int ROT = 0>
 __device__ __forceinline__ BFrag load_b_ahead(rsrc_t u, int chunk, int voff) {
-    if constexpr (XI < NP) return load_b(u, XI, chunk, voff);
-    else return load_b(u, XI - NP, (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
+    if constexpr (XI < NP) return load_b(u, pt<XI, ROT>(), chunk, voff);
+    else return load_b(u, pt<XI - NP, ROT>(), (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
 }
 
 // A fragments (V hi / lo of both row blocks) of one point
@@ -190,7 +199,7 @@ __device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
 
 // Point loop, software-pipelined: B PF points ahead (L2), A one point ahead (LDS).
 // The fold of point XI-1 is issued among point XI's MFMAs.
-template <int XI, int MODE, int PF>
+template <int XI, int MODE, int PF, int ROT = 0>
 __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag (&bq)[PF],
                                         AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff,
                                         AFrag *a_next = nullptr) {
@@ -202,45 +211,46 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
                 b2 = bq[0];
                 asm volatile("" : "+v"(b2.h), "+v"(b2.l));
             } else {
-                b2 = load_b_ahead<XI + PF>(u, chunk, voff);
+                b2 = load_b_ahead<XI + PF, ROT>(u, chunk, voff);
             }
             const BFrag b0 = bq[0];
-            if constexpr (MODE & kNoALookahead) a0 = load_a(sv, XI);  // this point's V, waited for here
+            if constexpr (MODE & kNoALookahead) a0 = load_a(sv, pt<XI, ROT>());  // this point's V, waited for here
             AFrag a1, a2;
             if constexpr (MODE & kALook2) {  // a_next holds point XI+1 (loaded a point ago); load XI+2
                 if constexpr (XI + 1 < NP) a1 = *a_next;
-                if constexpr (XI + 2 < NP) a2 = load_a(sv, XI + 2);
+                if constexpr (XI + 2 < NP) a2 = load_a(sv, pt<XI + 2, ROT>());
             } else if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) {
                 if constexpr (MODE & 16) {  // diagnostic: no A loads
                     a1 = a0;
                     asm volatile("" : "+v"(a1.h0), "+v"(a1.l0), "+v"(a1.h1), "+v"(a1.l1));
                 } else {
-                    a1 = load_a(sv, XI + 1);
+                    a1 = load_a(sv, pt<XI + 1, ROT>());
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
             floatx4 m0 = {}, m1 = {};
-            constexpr int srow = nth_row(XI / 5, 0) * 5 + XI % 5;  // the S row of a direct point
-            if constexpr (acc_direct<XI, MODE>()) {
+            constexpr int P = pt<XI, ROT>();
+            constexpr int srow = nth_row(P / 5, 0) * 5 + P % 5;  // the S row of a direct point
+            if constexpr (acc_direct<P, MODE>()) {
                 m0 = floatx4{S[srow].p[0].x, S[srow].p[0].y, S[srow].p[1].x, S[srow].p[1].y};
                 m1 = floatx4{S[srow].p[2].x, S[srow].p[2].y, S[srow].p[3].x, S[srow].p[3].y};
             }
             constexpr bool fold_here = XI > 0 && !(MODE & 64);
             // small terms first, then the hi x hi product
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h0, m0, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<XI - 1, 0, MODE>(S, mprev, k2, k4);
+            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 0, MODE>(S, mprev, k2, k4);
             m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h1, m1, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<XI - 1, 1, MODE>(S, mprev, k2, k4);
+            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 1, MODE>(S, mprev, k2, k4);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l0, m0, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<XI - 1, 2, MODE>(S, mprev, k2, k4);
+            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 2, MODE>(S, mprev, k2, k4);
             m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l1, m1, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<XI - 1, 3, MODE>(S, mprev, k2, k4);
+            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 3, MODE>(S, mprev, k2, k4);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h0, m0, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<XI - 1, 4, MODE>(S, mprev, k2, k4);
+            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 4, MODE>(S, mprev, k2, k4);
             m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<XI - 1, 5, MODE>(S, mprev, k2, k4);
+            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 5, MODE>(S, mprev, k2, k4);
             asm volatile("" : "+v"(m0), "+v"(m1));  // keep this point's MFMAs in its own region
-            if constexpr (acc_direct<XI, MODE>()) {
+            if constexpr (acc_direct<P, MODE>()) {
                 S[srow].p[0] = __builtin_shufflevector(m0, m0, 0, 1);
                 S[srow].p[1] = __builtin_shufflevector(m0, m0, 2, 3);
                 S[srow].p[2] = __builtin_shufflevector(m1, m1, 0, 1);
@@ -256,11 +266,11 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) a0 = a1;
             if constexpr ((MODE & kALook2) && XI + 2 < NP) *a_next = a2;
         }
-        if constexpr (XI == NP && !(MODE & 64)) fold_all<XI - 1, MODE>(S, mprev, k2, k4);  // nothing left to spread it over
+        if constexpr (XI == NP && !(MODE & 64)) fold_all<pt<XI - 1, ROT>(), MODE>(S, mprev, k2, k4);  // nothing left to spread it over
         if constexpr (XI < NP) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) mprev[i] = m[i];
-            xi_loop<XI + 1, MODE, PF>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff, a_next);
+            xi_loop<XI + 1, MODE, PF, ROT>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff, a_next);
         }
     }
 }
@@ -663,9 +673,11 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     }
     load_x<MODE>(xr, x, set_b0(0), n_boards, chunk_of(0), tid);
     SetScale sc = set_scale(x_amax, x_amax_per_board, set_b0(0), n_boards);  // V scales of the current set
+    // kStagger (diagnostic): waves 4-7 start their point walk at kStaggerRot
+    const int rot = ((MODE & kStagger) && wv >= 4) ? kStaggerRot : 0;
     BFrag bq[PF];
 #pragma unroll
-    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, c_rot, voff);
+    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, (i + rot) % NP, c_rot, voff);
     if constexpr (!(MODE & kSerialPrologue)) zero_pads();
     store_x(sX, xr, sc, tid);
     __syncthreads();
@@ -702,10 +714,11 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         mark(g, 2, t0);
         if constexpr ((MODE & 3) != 2) {
             AFrag a0, an;
-            if constexpr (!(MODE & kNoALookahead)) a0 = load_a(sv_lane, 0);
-            if constexpr (MODE & kALook2) an = load_a(sv_lane, 1);
+            if constexpr (!(MODE & kNoALookahead)) a0 = load_a(sv_lane, rot);
+            if constexpr (MODE & kALook2) an = load_a(sv_lane, (1 + rot) % NP);
             floatx2 mprev[4];
-            xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
+            if ((MODE & kStagger) && rot) xi_loop<0, MODE, PF, kStaggerRot>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
+            else xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         }
         mark(g, 3, t0);
         if (c == NCH - 1)
