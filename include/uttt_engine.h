@@ -92,8 +92,9 @@ int uttt_boltzman(const float *xs, int32_t n, float temperature, float *out);
 typedef struct uttt_engine uttt_engine_t;
 
 /* device: HIP ordinal (-1 = the calling thread's current device). max_trees: concurrent trees / game slots. max_sims: the
- * largest evaluate_count this engine will run (sizes the node pool to the
- * exact worst case 82 + 81*max_sims nodes per tree, so it cannot overflow). */
+ * largest evaluate_count this engine will run, 1..4095 (sizes the node pool to the
+ * exact worst case 82 + 81*max_sims nodes per tree, so it cannot overflow; the 16-byte node
+ * record holds visits and child-block counts up to 4095). */
 int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out);
 int uttt_engine_destroy(uttt_engine_t *eng);
 /* Launch everything on `stream` (a hipStream_t, e.g. torch's current stream;

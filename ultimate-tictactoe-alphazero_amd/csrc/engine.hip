@@ -1,12 +1,11 @@
 // engine.hip — batched PV-MCTS + self-play for MI355X (gfx950, wave64).
 //
-// Many independent PUCT trees live in flat SoA pools in HBM:
-//   N[i] (i32 visits), W[i] (f32 value sum), P[i] (f32 prior), LINK[i] (uint2:
-//   first child | k copies : 16, |legal| : 8, action : 8)
-// indexed t * cap + local, the root at local 0. A node's children are one
-// contiguous block of k*|legal| entries (k = copies of the flushed leaf,
-// uttt_mcts.cpp:121-135 + :38-43 append semantics), so PUCT reads 12 B per
-// child fully coalesced. States are never stored per node: a descent replays
+// Many independent PUCT trees live in flat pools in HBM, one 16-byte record per
+// node: {W f32 value sum, P f32 prior, meta (visits N : 16 | action : 7 | |legal| : 7
+// | 2 flags), link (first child : 20 | k copies : 12)}, indexed t * cap + local, the
+// root at local 0. A node's children are one contiguous block of k*|legal| records
+// (k = copies of the flushed leaf, uttt_mcts.cpp:121-135 + :38-43 append semantics),
+// so the PUCT scan reads one 16-byte record per child, fully coalesced. States are never stored per node: a descent replays
 // the actions from the root on bitboards (uttt_bits.h).
 //
 // One round (uttt_mcts.cpp:109-167, all trees in lock-step):
@@ -110,13 +109,18 @@ struct LeafRec {
     int32_t pad;
 };
 
+// One node (round 4: four SoA arrays N, W, P, LINK became one record, so the PUCT scan loads a child
+// with one dwordx4 and an expansion stores a child with one):
+//   .x W (f32 bits)   .y P (f32 bits)
+//   .z meta: visits N (bits 0-15) | action (16-22) | L = |legal| of the node's state, the size of
+//      each of its child blocks (23-29) | kMetaP64 (30) | kMetaWF32 (31)
+//   .w link: first child (bits 0-19) | k = its child blocks (20-31)
+// Limits: max_sims <= 4095 (k and N fit; the pool cap 82 + 81 * max_sims < 2^20 first-child indices).
 struct Pool {
-    int32_t *n;
-    float *w;
-    float *p;
-    uint2 *link;
+    uint4 *rec;
     int64_t cap;
 };
+constexpr int kMaxSimsRec = 4095;
 
 struct Trees {
     TreeCtl *ctl;
@@ -134,16 +138,24 @@ struct Trees {
     int32_t py;  // 1: pv_mcts.py semantics (arena), 0: cpp/uttt_mcts.cpp (self-play)
 };
 
-// link.y packing
-__host__ __device__ __forceinline__ uint32_t pack_meta(uint32_t k, uint32_t L, uint32_t action) {
-    return (k & 0xFFFFu) | ((L & 0xFFu) << 16) | ((action & 0xFFu) << 24);
+// record packing (Pool)
+constexpr uint32_t kNoAction = 0x7Fu;
+__host__ __device__ __forceinline__ uint32_t make_meta(uint32_t action, uint32_t L) {  // N = 0
+    return ((action & 0x7Fu) << 16) | ((L & 0x7Fu) << 23);
 }
-__host__ __device__ __forceinline__ int meta_k(uint32_t y) { return (int)(y & 0x3FFFu); }
+__host__ __device__ __forceinline__ int meta_n(uint32_t m) { return (int)(m & 0xFFFFu); }
+__host__ __device__ __forceinline__ int meta_action(uint32_t m) { return (int)((m >> 16) & 0x7Fu); }
+__host__ __device__ __forceinline__ int meta_L(uint32_t m) { return (int)((m >> 23) & 0x7Fu); }
 // py semantics only (pv_mcts.py, NumPy 2 scalar promotion):
-constexpr uint32_t kMetaP64 = 0x4000u;   // this node's children carry float64 uniform priors
-constexpr uint32_t kMetaWF32 = 0x8000u;  // this node's w has become np.float32 (a network value)
-__host__ __device__ __forceinline__ int meta_L(uint32_t y) { return (int)((y >> 16) & 0xFFu); }
-__host__ __device__ __forceinline__ int meta_action(uint32_t y) { return (int)(y >> 24); }
+constexpr uint32_t kMetaP64 = 1u << 30;   // this node's children carry float64 uniform priors
+constexpr uint32_t kMetaWF32 = 1u << 31;  // this node's w has become np.float32 (a network value)
+constexpr uint32_t kMetaLMask = 0x7Fu << 23;
+__host__ __device__ __forceinline__ uint32_t make_link(uint32_t first, uint32_t k) { return (first & 0xFFFFFu) | (k << 20); }
+__host__ __device__ __forceinline__ int link_first(uint32_t l) { return (int)(l & 0xFFFFFu); }
+__host__ __device__ __forceinline__ int link_k(uint32_t l) { return (int)(l >> 20); }
+__device__ __forceinline__ uint4 new_child(float p, uint32_t action) {
+    return make_uint4(0u, __float_as_uint(p), make_meta(action, 0u), 0u);
+}
 
 // ------------------------------------------------------------ wave helpers --
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
@@ -511,43 +523,34 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     const bool p64 = py && !(sum > 0);  // np.ones(float) / L: float64 priors
     const float q0 = sum > 0 ? p0 / sum : un;
     const float q1 = sum > 0 ? p1 / sum : un;
+    const uint4 c0 = new_child(q0, (uint32_t)lane), c1 = new_child(q1, (uint32_t)(64 + lane));
     for (int j = 0; j < blocks; ++j) {
         const size_t blk = base + nb + (size_t)j * L;
-        if (l0) {
-            pool.n[blk + i0] = 0;
-            pool.w[blk + i0] = 0.0f;
-            pool.p[blk + i0] = q0;
-            pool.link[blk + i0] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
-        }
-        if (l1) {
-            pool.n[blk + i1] = 0;
-            pool.w[blk + i1] = 0.0f;
-            pool.p[blk + i1] = q1;
-            pool.link[blk + i1] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
-        }
+        if (l0) pool.rec[blk + i0] = c0;
+        if (l1) pool.rec[blk + i1] = c1;
     }
-    if (lane <= depth) {
-        float w = pool.w[base + path_lo];
-        const float x = ((depth - lane) & 1) ? -v : v;
+    // the path, leaf (lane depth) to root: w += v k times with the sign flipping upwards, N += k; the
+    // leaf also gets its children's block size L and its link (first child, k copies: cpp k blocks,
+    // py one block); py: every node on the path now holds a float32 w (kMetaWF32), and the leaf's
+    // children carry float64 priors when the policy summed to zero (kMetaP64)
+    const uint32_t leaf_meta = (uint32_t)L << 23 | (py ? (kMetaWF32 | (p64 ? kMetaP64 : 0u)) : 0u);
+    const uint32_t leaf_link = make_link((uint32_t)nb, (uint32_t)k);
+    auto update = [&](int pn, int d) {  // path node pn at depth d
+        uint4 r = pool.rec[base + pn];
+        float w = __uint_as_float(r.x);
+        const float x = ((depth - d) & 1) ? -v : v;
         for (int j = 0; j < k; ++j) w += x;
-        pool.w[base + path_lo] = w;
-        pool.n[base + path_lo] += k;
-        if (py && lane < depth) pool.link[base + path_lo].y |= kMetaWF32;
-    }
-    if (lane + 64 <= depth) {
-        float w = pool.w[base + path_hi];
-        const float x = ((depth - lane - 64) & 1) ? -v : v;
-        for (int j = 0; j < k; ++j) w += x;
-        pool.w[base + path_hi] = w;
-        pool.n[base + path_hi] += k;
-        if (py && lane + 64 < depth) pool.link[base + path_hi].y |= kMetaWF32;
-    }
-    if (lane == 0) {
-        const uint2 old = pool.link[base + node];
-        uint32_t meta = pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y));
-        if (py) meta |= kMetaWF32 | (p64 ? kMetaP64 : 0u);
-        pool.link[base + node] = make_uint2((uint32_t)nb, meta);
-    }
+        r.x = __float_as_uint(w);
+        r.z += (uint32_t)k;
+        if (py && d < depth) r.z |= kMetaWF32;
+        if (d == depth) {
+            r.z = (r.z & ~kMetaLMask) | leaf_meta;
+            r.w = leaf_link;
+        }
+        pool.rec[base + pn] = r;
+    };
+    if (lane <= depth) update(path_lo, lane);
+    if (lane + 64 <= depth) update(path_hi, lane + 64);
     node_count = nb + blocks * L;
     return true;
 }
@@ -567,10 +570,7 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
     if (tr.py) {  // pv_mcts.py:134: the root is a plain unexpanded node (evaluated by the first flush)
         const bool any = __ballot(bit_of(m, lane) != 0u) != 0ull || __ballot(lane < 17 && bit_of(m, 64 + lane) != 0u);
         if (lane == 0) {
-            pool.n[base] = 0;
-            pool.w[base] = 0.0f;
-            pool.p[base] = 0.0f;
-            pool.link[base] = make_uint2(0u, pack_meta(0, 0, 0xFFu));
+            pool.rec[base] = make_uint4(0u, 0u, make_meta(kNoAction, 0u), 0u);
             tr.root[t] = s;
             TreeCtl c;
             c.sims_done = 0;
@@ -586,25 +586,10 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
     const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
     const int L = __popcll(b0) + __popcll(b1);
     const float up = L ? 1.0f / (float)L : 0.0f;
-    if (l0) {
-        const int i = 1 + __popcll(b0 & lanes_below());
-        pool.n[base + i] = 0;
-        pool.w[base + i] = 0.0f;
-        pool.p[base + i] = up;
-        pool.link[base + i] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
-    }
-    if (l1) {
-        const int i = 1 + __popcll(b0) + __popcll(b1 & lanes_below());
-        pool.n[base + i] = 0;
-        pool.w[base + i] = 0.0f;
-        pool.p[base + i] = up;
-        pool.link[base + i] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
-    }
+    if (l0) pool.rec[base + 1 + __popcll(b0 & lanes_below())] = new_child(up, (uint32_t)lane);
+    if (l1) pool.rec[base + 1 + __popcll(b0) + __popcll(b1 & lanes_below())] = new_child(up, (uint32_t)(64 + lane));
     if (lane == 0) {
-        pool.n[base] = 0;
-        pool.w[base] = 0.0f;
-        pool.p[base] = 0.0f;
-        pool.link[base] = make_uint2(L ? 1u : 0u, pack_meta(L ? 1 : 0, (uint32_t)L, 0xFFu));
+        pool.rec[base] = make_uint4(0u, 0u, make_meta(kNoAction, (uint32_t)L), make_link(L ? 1u : 0u, L ? 1u : 0u));
         tr.root[t] = s;
         TreeCtl c;
         c.sims_done = 0;
@@ -648,8 +633,8 @@ enum SelPhase {
     kSpQueue,       // pending-leaf record
     kSpCount
 };
-constexpr int kSelHeavyTrips = 24;
 #ifdef UTTT_DIAG_BUILD
+constexpr int kSelHeavyTrips = 24;
 __device__ unsigned long long g_sel_cyc[2 * kSpCount + 2];  // [all trees][heavy trees], then tree counts
 struct SelClock {
     unsigned long long t, acc[kSpCount];
@@ -696,30 +681,21 @@ struct SelClock {
 // another behind per-child branches. Children past cnt (clamped loads) never win; the compare is the
 // reference's strict '>' in child order.
 template <int NJ>
-__device__ __forceinline__ void puct_group(const int32_t *__restrict__ N, const float *__restrict__ W,
-                                           const float *__restrict__ P, const uint2 *__restrict__ LK, int first,
-                                           int c0, int cnt, float sq, int lane, float &best, int &bi, int &bn,
-                                           uint2 &bl, SelClock &clk) {
-    int cn[NJ];
-    float cw[NJ], cp[NJ];
-    uint2 cl[NJ];
+__device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int first, int c0, int cnt, float sq, int lane,
+                                           float &best, int &bi, uint2 &bl, SelClock &clk) {
+    uint4 r[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int c = min(c0 + j * kWave + lane, cnt - 1);
-        cn[j] = N[first + c];
-        cw[j] = W[first + c];
-        cp[j] = P[first + c];
-        cl[j] = LK[first + c];
-    }
+    for (int j = 0; j < NJ; ++j) r[j] = R[first + min(c0 + j * kWave + lane, cnt - 1)];
     clk.mark<kSpLoad>();
     float v[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         // uttt_mcts.cpp:70-72, same association and rounding (no FMA: -ffp-contract=off); the
         // reference divides only when n > 0, and an unvisited child's quotient here is discarded
-        const float qd = -cw[j] / (float)max(cn[j], 1);
-        const float q = cn[j] > 0 ? qd : 0.0f;
-        const float u = cp[j] * sq / (float)(1 + cn[j]);
+        const int cn = meta_n(r[j].z);
+        const float qd = -__uint_as_float(r[j].x) / (float)max(cn, 1);
+        const float q = cn > 0 ? qd : 0.0f;
+        const float u = __uint_as_float(r[j].y) * sq / (float)(1 + cn);
         v[j] = q + u;
     }
 #pragma unroll
@@ -728,9 +704,8 @@ __device__ __forceinline__ void puct_group(const int32_t *__restrict__ N, const 
         const bool take = c < cnt && v[j] > best;
         best = take ? v[j] : best;
         bi = take ? c : bi;
-        bn = take ? cn[j] : bn;
-        bl.x = take ? cl[j].x : bl.x;
-        bl.y = take ? cl[j].y : bl.y;
+        bl.x = take ? r[j].z : bl.x;  // the winner's meta (visits, action, L) and link
+        bl.y = take ? r[j].w : bl.y;
     }
     clk.mark<kSpPuct>();
 }
@@ -754,10 +729,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     clk.start();
     if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
         const size_t base = (size_t)t * pool.cap;
-        int32_t *__restrict__ N = pool.n + base;
-        float *__restrict__ W = pool.w + base;
-        const float *__restrict__ P = pool.p + base;
-        const uint2 *__restrict__ LK = pool.link + base;
+        uint4 *__restrict__ R = pool.rec + base;
         const uttt_state_t root = tr.root[t];
         int sims_done = ctl.sims_done;
         int budget = kSelectBudget;
@@ -765,22 +737,22 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             uttt_state_t s = root;
             int node = 0, depth = 0;
             int path_lo = 0, path_hi = 0;  // lane d: path[d], path[64 + d]
-            uint2 lk = LK[0];
-            int node_n = N[0];  // the current node's visits (below the root: from the parent's scan)
+            // the current node's meta (visits, action, L) and link (below the root: from the parent's scan)
+            const uint4 r0 = R[0];
+            uint2 nm = make_uint2(r0.z, r0.w);
             ++trips;
             clk.mark<kSpRoot>();
             bool fail = false;
             for (;;) {
-                const int cnt = PY ? meta_L(lk.y) : meta_k(lk.y) * meta_L(lk.y);
+                const int cnt = PY ? meta_L(nm.x) : link_k(nm.y) * meta_L(nm.x);
                 if (cnt == 0) break;
-                const int first = (int)lk.x;
-                const int kself = (node == 0 && !PY) ? 0 : meta_k(lk.y);
+                const int first = link_first(nm.y);
+                const int kself = (node == 0 && !PY) ? 0 : link_k(nm.y);
+                const int total = meta_n(nm.x) - kself;  // == sum of children's visits
                 int bi = kNone;
                 if (!PY) {
-                    const int total = node_n - kself;  // == sum of children's visits
                     const float sq = sqrtf((float)total);
                     float best = -1e9f;
-                    int bn = 0;
                     uint2 bl = make_uint2(0u, 0u);
                     // Every load of a group of kScanGroup x 64 children is issued before the first
                     // compare (one memory round trip per group; a node expanded by a flush of k = 8
@@ -789,39 +761,38 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
                         ++trips;
-                        if (cnt - c0 <= kWave) puct_group<1>(N, W, P, LK, first, c0, cnt, sq, lane, best, bi, bn, bl, clk);
-                        else puct_group<kScanGroup>(N, W, P, LK, first, c0, cnt, sq, lane, best, bi, bn, bl, clk);
+                        if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bl, clk);
+                        else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bl, clk);
                     }
                     bi = __builtin_amdgcn_readlane(wave_argmax_to63(best, bi), 63);
-                    if (bi != kNone) {  // the winner's lane holds its visits and link word
+                    if (bi != kNone) {  // the winner's lane holds its meta and link words
                         const int wl = bi & (kWave - 1);
-                        node_n = __builtin_amdgcn_readlane(bn, wl);
-                        lk = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)bl.x, wl),
+                        nm = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)bl.x, wl),
                                         (uint32_t)__builtin_amdgcn_readlane((int)bl.y, wl));
                     }
                     clk.mark<kSpArgmax>();
                 } else {
-                    const int total = N[node] - kself;  // == sum of children's visits
-                    trips += 2u + (unsigned int)((cnt + kWave - 1) / kWave);  // N[node], the scan, LK[node]
+                    trips += 2u + (unsigned int)((cnt + kWave - 1) / kWave);  // the node's record, the scan
                     // pv_mcts.py:120-130 under NumPy 2 promotion: float32 ops with sqrt(t)
                     // in double, or float64 throughout when the priors are float64;
                     // np.argmax: first maximum, a NaN counts as the maximum.
-                    const bool p64 = (lk.y & kMetaP64) != 0u;
+                    const bool p64 = (nm.x & kMetaP64) != 0u;
                     const double sqt = sqrt((double)total);
                     const float sq = (float)sqt;
-                    const double pu = 1.0 / (double)meta_L(lk.y);
+                    const double pu = 1.0 / (double)meta_L(nm.x);
                     double best = -HUGE_VAL;
                     for (int c = lane; c < cnt; c += kWave) {
-                        const int cn = N[first + c];
-                        const float cw = W[first + c];
-                        const bool wf = (LK[first + c].y & kMetaWF32) != 0u;
+                        const uint4 rc = R[first + c];
+                        const int cn = meta_n(rc.z);
+                        const float cw = __uint_as_float(rc.x);
+                        const bool wf = (rc.z & kMetaWF32) != 0u;
                         double v;
                         if (p64) {
                             const double q = cn > 0 ? (wf ? (double)((-cw) / (float)cn) : (double)(-cw) / (double)cn) : 0.0;
                             v = q + ((1.0 * pu) * sqt) / (double)(1 + cn);
                         } else {
                             const float q = cn > 0 ? (wf ? (-cw) / (float)cn : (float)((double)(-cw) / (double)cn)) : 0.0f;
-                            const float u = ((1.0f * P[first + c]) * sq) / (float)(1 + cn);
+                            const float u = ((1.0f * __uint_as_float(rc.y)) * sq) / (float)(1 + cn);
                             v = (double)(q + u);
                         }
                         if (v != v) v = HUGE_VAL;
@@ -850,8 +821,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     if (depth < 64) path_lo = node;
                     else path_hi = node;
                 }
-                if (PY) lk = LK[node];
-                s = next_state(s, meta_action(lk.y));
+                if (PY) {
+                    const uint4 rn = R[node];
+                    nm = make_uint2(rn.z, rn.w);
+                }
+                s = next_state(s, meta_action(nm.x));
                 clk.mark<kSpNext>();
             }
             if (fail) break;
@@ -863,16 +837,14 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
                 // backpropagate adds it at the leaf and flips sign upwards (:47-54).
                 const float v = -(lose ? -1.0f : 0.0f);
-                if (lane <= depth) {
-                    const float x = ((depth - lane) & 1) ? -v : v;
-                    W[path_lo] += x;
-                    N[path_lo] += 1;
-                }
-                if (lane + 64 <= depth) {
-                    const float x = ((depth - lane - 64) & 1) ? -v : v;
-                    W[path_hi] += x;
-                    N[path_hi] += 1;
-                }
+                auto backup1 = [&](int pn, int d) {
+                    uint4 r = R[pn];
+                    r.x = __float_as_uint(__uint_as_float(r.x) + (((depth - d) & 1) ? -v : v));
+                    r.z += 1u;
+                    R[pn] = r;
+                };
+                if (lane <= depth) backup1(path_lo, lane);
+                if (lane + 64 <= depth) backup1(path_hi, lane + 64);
                 wave_memory_fence();
                 trips += 2;
                 bytes += 16ull * (unsigned long long)(depth + 1);
@@ -904,7 +876,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 clk.mark<kSpExpand>();
                 wave_memory_fence();
                 if (lane == 0) atomicAdd(stripe_of(cache.ctr), 1ull);
-                bytes += 20ull * (unsigned long long)(k * meta_L(LK[node].y)) + 16ull * (depth + 1);
+                bytes += 20ull * (unsigned long long)(k * (int)legal_count(s)) + 16ull * (depth + 1);
                 clk.mark<kSpHitTail>();
                 sims_done += k;
                 if (sims_done >= tr.sims) break;
@@ -1148,8 +1120,9 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             }
             return;
         }
-        float w_lo = lane <= depth ? pool.w[base + pn_lo] : 0.0f;
-        float w_hi = lane + 64 <= depth ? pool.w[base + pn_hi] : 0.0f;
+        uint4 r_lo = lane <= depth ? pool.rec[base + pn_lo] : make_uint4(0u, 0u, 0u, 0u);
+        uint4 r_hi = lane + 64 <= depth ? pool.rec[base + pn_hi] : make_uint4(0u, 0u, 0u, 0u);
+        float w_lo = __uint_as_float(r_lo.x), w_hi = __uint_as_float(r_hi.x);
         for (int j = 0; j < k; ++j) {
             const int64_t row = (int64_t)rowbase[slot] + j;
             const float *pol = policy + row * pld;
@@ -1162,35 +1135,24 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             const float q0 = sum > 0 ? p0 / sum : un;
             const float q1 = sum > 0 ? p1 / sum : un;
             const size_t blk = base + nb + (size_t)j * L;
-            if (l0) {
-                pool.n[blk + i0] = 0;
-                pool.w[blk + i0] = 0.0f;
-                pool.p[blk + i0] = q0;
-                pool.link[blk + i0] = make_uint2(0u, pack_meta(0, 0, (uint32_t)lane));
-            }
-            if (l1) {
-                pool.n[blk + i1] = 0;
-                pool.w[blk + i1] = 0.0f;
-                pool.p[blk + i1] = q1;
-                pool.link[blk + i1] = make_uint2(0u, pack_meta(0, 0, (uint32_t)(64 + lane)));
-            }
+            if (l0) pool.rec[blk + i0] = new_child(q0, (uint32_t)lane);
+            if (l1) pool.rec[blk + i1] = new_child(q1, (uint32_t)(64 + lane));
             const float v = value[row * vld];
             if (lane <= depth) w_lo += ((depth - lane) & 1) ? -v : v;
             if (lane + 64 <= depth) w_hi += ((depth - lane - 64) & 1) ? -v : v;
         }
-        if (lane <= depth) {
-            pool.w[base + pn_lo] = w_lo;
-            pool.n[base + pn_lo] += k;
-        }
-        if (lane + 64 <= depth) {
-            pool.w[base + pn_hi] = w_hi;
-            pool.n[base + pn_hi] += k;
-        }
-        if (lane == 0) {
-            const uint2 old = pool.link[base + r.node];
-            pool.link[base + r.node] =
-                make_uint2((uint32_t)nb, pack_meta((uint32_t)k, (uint32_t)L, (uint32_t)meta_action(old.y)));
-        }
+        // path nodes: w, N += k; the leaf (depth) also gets L and its link (first child, k blocks)
+        auto put = [&](uint4 rr, float w, int pn, int d) {
+            rr.x = __float_as_uint(w);
+            rr.z += (uint32_t)k;
+            if (d == depth) {
+                rr.z = (rr.z & ~kMetaLMask) | ((uint32_t)L << 23);
+                rr.w = make_link((uint32_t)nb, (uint32_t)k);
+            }
+            pool.rec[base + pn] = rr;
+        };
+        if (lane <= depth) put(r_lo, w_lo, pn_lo, lane);
+        if (lane + 64 <= depth) put(r_hi, w_hi, pn_hi, lane + 64);
         ctl.node_count = nb + k * L;
     }
     if (lane == 0) {
@@ -1228,10 +1190,11 @@ __global__ __launch_bounds__(kBlock) void k_hash_eval(const float *__restrict__ 
 
 // ---------------------------------------------------------- root results --
 __device__ __forceinline__ int root_children(const Pool &pool, size_t base, int &first) {
-    const uint2 lk = pool.link[base];
-    first = (int)lk.x;
-    return meta_L(lk.y);
+    const uint4 r = pool.rec[base];
+    first = link_first(r.w);
+    return meta_L(r.z);
 }
+__device__ __forceinline__ int visits_of(const Pool &pool, size_t i) { return meta_n(pool.rec[i].z); }
 
 // pv_mcts_scores' return value (uttt_mcts.cpp:177-195): root child visits as
 // f32 -> one-hot first max (t == 0) or boltzman (:199-216).
@@ -1240,9 +1203,9 @@ __device__ void root_scores(const Pool &pool, size_t base, float temperature, fl
     L = root_children(pool, base, first);
     if (temperature == 0.0f) {
         int mi = 0;
-        float mv = L ? (float)pool.n[base + first] : 0.0f;
+        float mv = L ? (float)visits_of(pool, base + first) : 0.0f;
         for (int i = 1; i < L; ++i) {
-            const float v = (float)pool.n[base + first + i];
+            const float v = (float)visits_of(pool, base + first + i);
             if (v > mv) {
                 mv = v;
                 mi = i;
@@ -1256,7 +1219,7 @@ __device__ void root_scores(const Pool &pool, size_t base, float temperature, fl
         const double y = (double)(1.0f / temperature);
         float sum = 0.0f;
         for (int i = 0; i < L; ++i) {
-            sc[i] = (float)pow((double)pool.n[base + first + i], y);
+            sc[i] = (float)pow((double)visits_of(pool, base + first + i), y);
             sum += sc[i];
         }
         if (sum > 0)
@@ -1300,7 +1263,7 @@ __global__ void k_root_visits(Pool pool, Trees tr, int32_t *visits, int32_t *n_l
     const size_t base = (size_t)t * pool.cap;
     int first;
     const int L = root_children(pool, base, first);
-    visits[g] = i < L ? pool.n[base + first + i] : 0;
+    visits[g] = i < L ? visits_of(pool, base + first + i) : 0;
     if (i == 0) n_legal[t] = L;
 }
 
@@ -1487,9 +1450,9 @@ __global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const u
     const int L = root_children(pool, base, first);
     if (sp.temperature == 0.0f) {
         int mi = 0;
-        float mv = L ? (float)pool.n[base + first] : 0.0f;
+        float mv = L ? (float)visits_of(pool, base + first) : 0.0f;
         for (int i = 1; i < L; ++i) {
-            const float v = (float)pool.n[base + first + i];
+            const float v = (float)visits_of(pool, base + first + i);
             if (v > mv) {
                 mv = v;
                 mi = i;
@@ -1501,7 +1464,7 @@ __global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const u
         float sum = 0.0f;
         for (int i = 0; i < L; ++i) {
             // pow(x, 1) == x exactly (IEEE 754): the self-play temperature 1.0 skips the call
-            const double xn = (double)pool.n[base + first + i];
+            const double xn = (double)visits_of(pool, base + first + i);
             const float v = (float)(y == 1.0 ? xn : pow(xn, y));
             pt[(i) * 64] = (double)v;
             sum += v;
@@ -1848,10 +1811,10 @@ extern "C" {
 const char *uttt_version(void) { return "uttt-mi355x 0.1 (gfx950)"; }
 
 int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt_engine_t **out) {
-    if (!out || max_trees <= 0 || max_trees >= (1 << 21) || max_sims <= 0 || max_sims > 60000) {
+    if (!out || max_trees <= 0 || max_trees >= (1 << 21) || max_sims <= 0 || max_sims > kMaxSimsRec) {
         // (k_scan packs its three per-round counts into 21-bit fields)
-        set_error("uttt_engine_create: bad arguments (max_trees=%d of at most 2097151, max_sims=%d)", max_trees,
-                  max_sims);
+        set_error("uttt_engine_create: bad arguments (max_trees=%d of at most 2097151, max_sims=%d of at most %d)",
+                  max_trees, max_sims, kMaxSimsRec);
         return UTTT_ERR_ARG;
     }
     int ndev = 0;
@@ -1885,9 +1848,7 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     e->stream = e->own_stream;
     const size_t nodes = (size_t)max_trees * (size_t)e->cap;
     e->pool.cap = e->cap;
-    if ((rc = alloc_n(e, &e->pool.n, nodes)) || (rc = alloc_n(e, &e->pool.w, nodes)) ||
-        (rc = alloc_n(e, &e->pool.p, nodes)) || (rc = alloc_n(e, &e->pool.link, nodes)))
-        return fail(rc);
+    if ((rc = alloc_n(e, &e->pool.rec, nodes))) return fail(rc);
     if ((rc = alloc_n(e, &e->tr.ctl, max_trees)) || (rc = alloc_n(e, &e->tr.root, max_trees)) ||
         (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
