@@ -635,7 +635,11 @@ enum SelPhase {
 };
 #ifdef UTTT_DIAG_BUILD
 constexpr int kSelHeavyTrips = 24;
-__device__ unsigned long long g_sel_cyc[2 * kSpCount + 2];  // [all trees][heavy trees], then tree counts
+// per tree (plain read-modify-writes by the tree's own wave: no same-address atomics, which would
+// serialize thousands of waves and distort the very latencies measured): [all launches' phases]
+// [heavy launches' phases][launches, heavy launches]
+constexpr int kSelDiagTrees = 8192;
+__device__ unsigned long long g_sel_cyc[kSelDiagTrees][2 * kSpCount + 2];
 struct SelClock {
     unsigned long long t, acc[kSpCount];
     __device__ __forceinline__ void start() {
@@ -652,15 +656,17 @@ struct SelClock {
         t = n;
     }
     __device__ __forceinline__ void flush(unsigned int trips) {
-        if ((threadIdx.x & 63) != 0) return;
+        const int tree = (int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+        if ((threadIdx.x & 63) != 0 || tree >= kSelDiagTrees) return;
+        unsigned long long *row = g_sel_cyc[tree];
         const int h = trips >= (unsigned int)kSelHeavyTrips;
 #pragma unroll
         for (int i = 0; i < kSpCount; ++i) {
-            atomicAdd(&g_sel_cyc[i], acc[i]);
-            if (h) atomicAdd(&g_sel_cyc[kSpCount + i], acc[i]);
+            row[i] += acc[i];
+            if (h) row[kSpCount + i] += acc[i];
         }
-        atomicAdd(&g_sel_cyc[2 * kSpCount], 1ull);
-        if (h) atomicAdd(&g_sel_cyc[2 * kSpCount + 1], 1ull);
+        row[2 * kSpCount] += 1ull;
+        if (h) row[2 * kSpCount + 1] += 1ull;
     }
 };
 #else
@@ -2562,12 +2568,20 @@ int uttt_engine_kernel_stats(uttt_engine_t *e, int32_t kernel, double *total_ms,
 }
 
 #ifdef UTTT_DIAG_BUILD
-// Diagnostics engine build only: k_select's phase cycles (SelClock), out[2 * kSpCount + 2]; reset zeroes them.
+// Diagnostics engine build only: k_select's phase cycles (SelClock) summed over the first kSelDiagTrees
+// trees, out[2 * kSpCount + 2]; reset zeroes them.
 int uttt_diag_select_cycles(unsigned long long *out, int32_t reset) {
-    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_cyc), sizeof(g_sel_cyc)) != hipSuccess) return UTTT_ERR_HIP;
+    static unsigned long long host[kSelDiagTrees][2 * kSpCount + 2];
+    if (out) {
+        if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sel_cyc), sizeof(host)) != hipSuccess) return UTTT_ERR_HIP;
+        for (int j = 0; j < 2 * kSpCount + 2; ++j) {
+            out[j] = 0ull;
+            for (int t = 0; t < kSelDiagTrees; ++t) out[j] += host[t][j];
+        }
+    }
     if (reset) {
-        static const unsigned long long zero[2 * kSpCount + 2] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_cyc), zero, sizeof(zero)) != hipSuccess) return UTTT_ERR_HIP;
+        memset(host, 0, sizeof(host));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_cyc), host, sizeof(host)) != hipSuccess) return UTTT_ERR_HIP;
     }
     return UTTT_OK;
 }
