@@ -329,7 +329,7 @@ __global__ __launch_bounds__(NT) void k_wino3p_conv(const float *__restrict__ x,
         }
         // the set's results leave before the next chunk's inputs are requested: the DMA below is
         // then the youngest op the next chunk's column-1 vmcnt wait must cover
-        if (c == NCH - 1) set_epilogue<RES, 0>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane);
+        if (c == NCH - 1) set_epilogue<RES, kFoldAT>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane);
         lds_barrier();  // column 4 of this chunk read by every wave: its slots take the next chunk's
         if (tr) col_all<4>(ti);
         lds_barrier();  // the next chunk's V complete; its staged inputs no longer read

@@ -62,6 +62,7 @@ constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS lat
 constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
 constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
+constexpr int kFoldAT = 1 << 18;          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
 constexpr int kStagger = 1 << 30;         // waves 4-7 walk the 25 points from kStaggerRot on (their SIMD partners
                                           // from 0), so the partners' fold-free and fold-heavy points interleave
 constexpr int kStaggerRot = 12;
@@ -81,17 +82,38 @@ __host__ __device__ constexpr int nth_row(int u, int i) {
     return a;
 }
 
-// Points whose A^T column has one nonzero (u = 0 -> row 0, u = 4 -> row 2, both coefficient 1)
-// accumulate straight into their S row as the MFMA's C operand: no fold ops for 10 of the 25
-// points (40 of 220 packed adds per chunk; 2-10% per launch, round 2)
+// The fold's transform along u (round 4). Rounds 1-3 accumulated S = A^T M. Any invertible Z gives
+// the same output through S' = (Z A^T) M, Y = (Z^-1 S') A, and Z = [c0 c1 c4]^-1 (ci the columns of
+// A^T) makes three of Z A^T's five columns unit vectors: points u = 0, 1, 4 (15 of 25) accumulate
+// straight into their S' row as the MFMA's C operand, and only u = 2, 3 are folded, with integer
+// coefficients (2, -1: exact scalings). Fold ops per chunk: 15 -> 10 folded points, 360 -> 240 f32 adds
+// per wave. Z^-1 = [[1,1,0],[0,1,0],[0,1,1]]: the epilogue restores S[0] = S'[0] + S'[1], S[2] = S'[2] + S'[1].
+__host__ __device__ constexpr int zat(int a, int u) {
+    constexpr int m[3][5] = {{1, 0, 2, -1, 0}, {0, 1, -1, 2, 0}, {0, 0, 2, 2, 1}};
+    return m[a][u];
+}
+template <int MODE>
+__host__ __device__ constexpr int fat(int a, int u) { return (MODE & kFoldAT) ? at(a, u) : zat(a, u); }
+template <int MODE>
+__host__ __device__ constexpr int f_rows(int u) { return (fat<MODE>(0, u) != 0) + (fat<MODE>(1, u) != 0) + (fat<MODE>(2, u) != 0); }
+template <int MODE>
+__host__ __device__ constexpr int f_nth(int u, int i) {
+    int a = 0;
+    for (; a < 3; ++a)
+        if (fat<MODE>(a, u) != 0 && i-- == 0) break;
+    return a;
+}
+
+// Points whose fold column has one nonzero (coefficient 1) accumulate straight into their S row as
+// the MFMA's C operand (round 2: u = 0 / 4 under A^T; round 4: u = 0 / 1 / 4 under Z A^T)
 template <int P, int MODE>
-__host__ __device__ constexpr bool acc_direct() { return n_rows(P / 5) == 1; }
+__host__ __device__ constexpr bool acc_direct() { return f_rows<MODE>(P / 5) == 1; }
 
 template <int P, int O, int MODE>
 __device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
     constexpr int u = P / 5, v = P % 5;
-    if constexpr (O < 4 * n_rows(u) && !acc_direct<P, MODE>()) {
-        constexpr int a = nth_row(u, O / 4), j = O % 4, K = at(a, u);
+    if constexpr (O < 4 * f_rows<MODE>(u) && !acc_direct<P, MODE>()) {
+        constexpr int a = f_nth<MODE>(u, O / 4), j = O % 4, K = fat<MODE>(a, u);
         // Inline asm is outside the compiler's hazard recognizer, so nothing pads these reads of
         // the previous point's MFMA results; the schedule keeps >= 6 instructions, one of them an
         // MFMA, between producer and reader, and the output bits equal those of a compiler-visible
@@ -143,7 +165,7 @@ __device__ __forceinline__ void fold_op(Acc (&S)[15], const floatx2 (&m)[4], flo
 constexpr int NSLOT = 6;  // MFMAs per point
 template <int P, int SL, int MODE, int O = 0>
 __device__ __forceinline__ void fold_slot(Acc (&S)[15], const floatx2 (&m)[4], floatx2 k2, floatx2 k4) {
-    constexpr int nops = 4 * n_rows(P / 5);
+    constexpr int nops = 4 * f_rows<MODE>(P / 5);
     if constexpr (O < nops) {
         if constexpr (O * NSLOT / nops == SL) fold_op<P, O, MODE>(S, m, k2, k4);
         fold_slot<P, SL, MODE, O + 1>(S, m, k2, k4);
@@ -230,7 +252,7 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
             __builtin_amdgcn_sched_barrier(0);
             floatx4 m0 = {}, m1 = {};
             constexpr int P = pt<XI, ROT>();
-            constexpr int srow = nth_row(P / 5, 0) * 5 + P % 5;  // the S row of a direct point
+            constexpr int srow = f_nth<MODE>(P / 5, 0) * 5 + P % 5;  // the S row of a direct point
             if constexpr (acc_direct<P, MODE>()) {
                 m0 = floatx4{S[srow].p[0].x, S[srow].p[0].y, S[srow].p[1].x, S[srow].p[1].y};
                 m1 = floatx4{S[srow].p[2].x, S[srow].p[2].y, S[srow].p[3].x, S[srow].p[3].y};
@@ -502,6 +524,15 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
         board_of[rt] = board;
         // this tile's board's V scale times su: both powers of two, so 1/x is exact
         inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
+    }
+    if constexpr (!(MODE & kFoldAT)) {  // S = Z^-1 S': rows 0 and 2 get row 1 added (both tile blocks)
+#pragma unroll
+        for (int v = 0; v < 5; ++v)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                S[v].p[j] = S[v].p[j] + S[5 + v].p[j];
+                S[10 + v].p[j] = S[10 + v].p[j] + S[5 + v].p[j];
+            }
     }
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
