@@ -101,7 +101,7 @@ class GraphedStep:
     caller's weights exactly as the eager loop does. The graph adds the step's loss to a device
     accumulator; batches of another size (an epoch's last) run the same body eagerly."""
 
-    def __init__(self, model, opt, x, p, v, batch_size, channels_last=False, precision="fp32"):
+    def __init__(self, model, opt, x, p, v, batch_size, channels_last=False, precision="fp32", tune=False):
         self.model, self.opt, self.x, self.p, self.v = model, opt, x, p, v
         self.channels_last = channels_last
         if precision not in PRECISIONS:
@@ -122,8 +122,16 @@ class GraphedStep:
         side.wait_stream(torch.cuda.current_stream(dev))
         # MIOpen's immediate mode (heuristic kernel choice), whatever torch.backends.cudnn.benchmark
         # says (the reference's dual_network.py sets it at import): with find mode the captured step
-        # ran 7x slower and trained to a different loss (round 3, tools/bench_train.py)
-        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=False):
+        # ran 7x slower and trained to a different loss (round 3, tools/bench_train.py). tune=True
+        # (round 4 experiment): MIOpen's find runs first in two eager steps outside any capture, and the
+        # warm-up and capture then reuse its choices (benchmark mode, results cached per shape)
+        if tune:
+            with torch.backends.cudnn.flags(enabled=True, benchmark=True, deterministic=False):
+                for _ in range(2):
+                    opt.zero_grad(set_to_none=True)
+                    self._body(self.idx)
+            torch.cuda.synchronize(dev)
+        with torch.backends.cudnn.flags(enabled=True, benchmark=bool(tune), deterministic=False):
             with torch.cuda.stream(side):
                 for _ in range(3):  # allocator, MIOpen kernel choice, optimiser state
                     opt.zero_grad(set_to_none=True)
@@ -190,7 +198,7 @@ def _use_graph(graph, device, world):
 
 
 def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, device=None, seed=0, lr=0.001,
-                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None):
+                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=False):
     """Train `model` (a DualNetwork) on `history` in place; returns the per-epoch mean losses.
     In a torch.distributed job every rank calls this with the same history and seed.
     graph (default on for one GPU; UTTT_TRAIN_GRAPH=0 disables): replay the step as a HIP graph
@@ -203,7 +211,7 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
         import os
         precision = os.environ.get("UTTT_TRAIN_PRECISION", "fp32")
     if _use_graph(graph, device, world):
-        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision)
+        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision, tune)
     if precision != "fp32":
         raise ValueError("precision other than fp32 needs the graph step (one GPU)")
     net = prepare(model, device, sync_bn)
@@ -229,7 +237,8 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
     return losses
 
 
-def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision="fp32"):
+def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision="fp32",
+                   tune=False):
     net = model.to(device)
     if channels_last:
         net = net.to(memory_format=torch.channels_last)
@@ -239,7 +248,7 @@ def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, ch
         opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, fused=True)
     else:
         opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, foreach=True)
-    step = GraphedStep(net, opt, x, p, v, batch_size, channels_last, precision)
+    step = GraphedStep(net, opt, x, p, v, batch_size, channels_last, precision, tune)
     losses = []
     for epoch in range(epochs):
         lr_t.fill_(lr * lr_lambda(epoch))
