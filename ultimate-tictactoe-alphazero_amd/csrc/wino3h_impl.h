@@ -62,7 +62,10 @@ constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS lat
 constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
 constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
-constexpr int kFoldAT = 1 << 18;          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
+constexpr int kFoldAT = 1 << 18;
+constexpr int kEarlyLoad = 1 << 19;       // the chunk-after-next's inputs requested at the end of this chunk's
+                                          // point GEMMs (before the barrier the earlier waves wait at), except
+                                          // after a set's last chunk (its epilogue needs the registers)          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
 constexpr int kStagger = 1 << 30;         // waves 4-7 walk the 25 points from kStaggerRot on (their SIMD partners
                                           // from 0), so the partners' fold-free and fold-heavy points interleave
 constexpr int kStaggerRot = 12;
@@ -733,7 +736,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         }
         // the next chunk's inputs load during this chunk's transform (registers are
         // free then; the point loop needs nearly all of them)
-        if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+        if (!(MODE & kEarlyLoad) || g == 0 || c == 0)
+            if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
         // the next chunk's V scales: this set's, or the next set's after its last chunk
         SetScale sc_next = sc;
         if (c == NCH - 1 && g + 1 < G) sc_next = set_scale(x_amax, x_amax_per_board, set_b0(g + 1), n_boards);
@@ -752,6 +756,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             else xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         }
         mark(g, 3, t0);
+        if constexpr (MODE & kEarlyLoad)
+            if (c != NCH - 1 && g + 2 < G) load_x<MODE>(xr, x, set_b0(g + 2), n_boards, chunk_of(g + 2), fresh(tid));
         if (c == NCH - 1)
             set_epilogue<RES, MODE>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, 0, s_bmax);
         sc = sc_next;
