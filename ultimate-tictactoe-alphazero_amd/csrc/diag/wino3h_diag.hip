@@ -129,6 +129,9 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
         case 75: UTTT_V(kFoldAT, 3); break;                // scalar fold along A^T (round-4 first step)
         case 76: UTTT_V(kEarlyLoad, 3); break;
         case 77: UTTT_V(kEarlyLoad | kBufferX, 3); break;
+        case 78: UTTT_V(kEpiBarrier, 3); break;
+        case 79: UTTT_V(kEpiPrio, 3); break;
+        case 80: UTTT_V(kEpiBarrier | kEarlyLoad, 3); break;
         case 71: UTTT_V(kBufferX, 3); break;
         case 72: UTTT_V(kBufferX, 4); break;
         case 73: UTTT_V(kStagger | kFoldPacked, 3); break;

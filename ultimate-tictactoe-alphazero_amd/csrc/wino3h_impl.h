@@ -63,6 +63,10 @@ constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before th
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
 constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
 constexpr int kFoldAT = 1 << 18;
+constexpr int kEpiBarrier = 1 << 7;       // a set's epilogue starts after every wave's last point GEMMs (a barrier):
+                                          // the earlier waves' epilogue VALU no longer takes the issue slots of
+                                          // their SIMD partners' last point GEMMs
+constexpr int kEpiPrio = 1 << 10;         // ... instead: waves 4-7 run a set's last point loop at s_setprio 1
 constexpr int kEarlyLoad = 1 << 19;       // the chunk-after-next's inputs requested at the end of this chunk's
                                           // point GEMMs (before the barrier the earlier waves wait at), except
                                           // after a set's last chunk (its epilogue needs the registers)          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
@@ -747,6 +751,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sc_next, fresh(tid));
         mark(g, 2, t0);
+        if constexpr (MODE & kEpiPrio)
+            if (c == NCH - 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
         if constexpr ((MODE & 3) != 2) {
             AFrag a0, an;
             if constexpr (!(MODE & kNoALookahead)) a0 = load_a(sv_lane, rot);
@@ -755,6 +761,10 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             if ((MODE & kStagger) && rot) xi_loop<0, MODE, PF, kStaggerRot>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
             else xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         }
+        if constexpr (MODE & kEpiPrio)
+            if (c == NCH - 1 && wv >= 4) __builtin_amdgcn_s_setprio(0);
+        if constexpr (MODE & kEpiBarrier)
+            if (c == NCH - 1) __builtin_amdgcn_s_barrier();
         mark(g, 3, t0);
         if constexpr (MODE & kEarlyLoad)
             if (c != NCH - 1 && g + 2 < G) load_x<MODE>(xr, x, set_b0(g + 2), n_boards, chunk_of(g + 2), fresh(tid));
