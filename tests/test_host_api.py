@@ -115,6 +115,16 @@ def test_engine_requires_gpu_loudly():
         Engine(4, 50)
 
 
+def test_engine_limits_are_checked_before_the_device(engine_lib):
+    """max_sims is bounded by the 16-byte node record (visits, child-block counts <= 4095): larger
+    requests are refused with UTTT_ERR_ARG and a message, before any device call."""
+    import ctypes
+    h = ctypes.c_void_p()
+    assert engine_lib.uttt_engine_create(-1, 4, 4096, ctypes.byref(h)) == -1
+    assert b"4095" in engine_lib.uttt_last_error()
+    assert engine_lib.uttt_engine_create(-1, 0, 50, ctypes.byref(h)) == -1
+
+
 def test_calibrated_network_reproduces_reference_fixture():
     """tests/golden/netcal.npz pins the non-saturated network the GPU parity tests use: the
     seed-0 DualNetwork + the fixture's BatchNorm statistics (uttt_amd.model.calibrated_network)
@@ -168,6 +178,14 @@ def test_winograd3_algebra_matches_direct_conv(engine_lib):
             V = np.einsum("ui,ijc,vj->uvc", BT, d, BT)
             M = np.einsum("uvc,uvco->uvo", V, U)
             y[3 * ty:3 * ty + 3, 3 * tx:3 * tx + 3] = np.einsum("au,uvo,bv->abo", AT, M, AT)
+            # the kernel's fold (round 4): S' = (Z A^T) M along u with Z = [c0 c1 c4]^-1, then
+            # S = Z^-1 S' in the epilogue; the same Y
+            ZAT = np.array([[1, 0, 2, -1, 0], [0, 1, -1, 2, 0], [0, 0, 2, 2, 1]], np.float64)
+            Zinv = np.array([[1, 1, 0], [0, 1, 0], [0, 1, 1]], np.float64)
+            assert np.array_equal(Zinv @ ZAT, AT)
+            S = np.einsum("za,avo->zvo", Zinv, np.einsum("au,uvo->avo", ZAT, M))
+            assert np.allclose(np.einsum("avo,bv->abo", S, AT), y[3 * ty:3 * ty + 3, 3 * tx:3 * tx + 3], rtol=1e-12,
+                               atol=1e-9)
     direct = np.zeros((9, 9, 128))
     for ky in range(3):
         for kx in range(3):
