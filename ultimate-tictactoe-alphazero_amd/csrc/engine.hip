@@ -243,31 +243,41 @@ constexpr int kCacheVal = 82;
 // and read as 16-byte agent-scope (sc1) accesses, 23 lanes of one wave: one fabric write per 16 B
 // instead of one per 4-byte store (MI355X_MICROARCH.md: narrow sc1 stores are one fabric write each).
 constexpr int kRecBytes = 384;
-constexpr int kRecKey = 0, kRecVal = 32;
+constexpr int kRecVal = 32;  // the key is the record's first 32 bytes
 constexpr int kRecLanes = 23;  // 16-byte pieces written per record: 2 of key, 21 of values
 constexpr int kSc1 = 16;       // buffer-intrinsic cache-policy bit: sc1 (agent scope)
 static_assert(kRecVal + 16 * (kRecLanes - 2) >= kRecVal + 4 * kCacheVal && 16 * kRecLanes <= kRecBytes, "record");
 
 struct EvalCache {
-    // 0 empty; odd: a writer holds the slot; even >= 2: ready. A writer claims by CAS from the value it
-    // saw to that + 1 and publishes that + 2, so every publish is a new version: a reader compares the
-    // flag it probed with the flag after its copy (a seqlock without ABA).
+    // Per slot one flag word: bits 0-15 a version (0 empty; odd: a writer holds the slot; even >= 2:
+    // ready), bits 16-31 the ready entry's tag (16 bits of its position's hash). A writer claims by
+    // CAS from the value it saw to that + 1 and publishes the version + 2 with the new tag, so every
+    // publish is a new flag value: a reader compares the flag it probed with the flag after its copy
+    // (a seqlock without ABA). Probes read only the flags (32 contiguous bytes for 8 slots) and
+    // load a record only for a ready slot whose tag matches (round 4: rounds 1-3 read 8 keys per probe).
     uint32_t *flag;
     char *rec;           // [slot][kRecBytes]
     uint32_t mask;       // capacity - 1
     unsigned long long *ctr;  // [0] hits, [1] misses (network leaves), [2] inserts, [3] replacements
 };
 
-__device__ __forceinline__ bool flag_ready(uint32_t f) { return f != 0u && !(f & 1u); }
-__device__ __forceinline__ uint32_t flag_next(uint32_t f) { return f + 2u == 0u ? 2u : f + 2u; }  // f even
+__device__ __forceinline__ bool flag_ready(uint32_t f) { return (f & 0xFFFFu) != 0u && !(f & 1u); }
+__device__ __forceinline__ uint32_t flag_tag(uint32_t f) { return f >> 16; }
+// the flag that publishes a slot claimed from flag f (f & 0xFFFF even, or 0 for an empty slot)
+__device__ __forceinline__ uint32_t flag_publish(uint32_t f, uint32_t tag) {
+    const uint32_t v = (f & 0xFFFFu) + 2u;
+    return (tag << 16) | (v > 0xFFFFu ? 2u : v);
+}
 
-__device__ __forceinline__ uint32_t state_hash(const uttt_state_t &s) {
+__device__ __forceinline__ uint64_t state_hash64(const uttt_state_t &s) {
     const uint64_t a = ((uint64_t)s.own[1] << 32) | s.own[0];
     const uint64_t b = ((uint64_t)s.opp[0] << 32) | s.own[2];
     const uint64_t c = ((uint64_t)s.opp[2] << 32) | s.opp[1];
     const uint64_t d = ((uint64_t)(uint32_t)s.active << 32) | s.mains;
-    return (uint32_t)mix64(mix64(mix64(mix64(kGold ^ a) ^ b) ^ c) ^ d);
+    return mix64(mix64(mix64(mix64(kGold ^ a) ^ b) ^ c) ^ d);
 }
+// a position's tag: the top 16 bits of its hash (its slot: the low 32 bits)
+__device__ __forceinline__ uint32_t state_tag(uint64_t h64) { return (uint32_t)(h64 >> 48); }
 
 __device__ __forceinline__ bool same_state(const uttt_state_t &x, const uttt_state_t &y) {
     return x.own[0] == y.own[0] && x.own[1] == y.own[1] && x.own[2] == y.own[2] && x.opp[0] == y.opp[0] &&
@@ -298,74 +308,61 @@ __device__ __forceinline__ rsrc_t rec_rsrc(const EvalCache &c, uint32_t slot) {
     return __builtin_amdgcn_make_buffer_rsrc(c.rec + (size_t)slot * kRecBytes, 0, kRecBytes, 0x00020000);
 }
 
-// this lane's probe of its own slot: the key as four 8-byte agent loads
-__device__ __forceinline__ bool key_is(const EvalCache &c, uint32_t slot, const uttt_state_t &s) {
-    const uint64_t *k = reinterpret_cast<const uint64_t *>(c.rec + (size_t)slot * kRecBytes + kRecKey);
-    const uint64_t *w = reinterpret_cast<const uint64_t *>(&s);
-    bool same = true;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) same &= ld_agent(k + i) == w[i];
-    return same;
-}
-
-// Wave-uniform lookup, the kProbe slots probed by lanes 0..kProbe-1 at once:
-// a hit counts only if no empty slot precedes it in probe order. On a hit the
-// 82 values are copied to dst (LDS, 16-byte aligned, >= 84 floats) and true is returned.
+// Wave-uniform lookup: lanes 0..kProbe-1 read the kProbe slots' flags at once; the first ready slot
+// whose tag matches (a hit counts only if no empty slot precedes it in probe order) has its whole
+// record read in one round trip (lanes 0-1 the key, checked against s; 2-22 the values), then the
+// flag is re-checked. On a hit the 82 values are copied to dst (LDS, 16-byte aligned, >= 84 floats)
+// and true is returned; a tag that matched another position's entry (a 16-bit collision) is a miss.
 __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *dst) {
     if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
-    const uint32_t h = state_hash(s);
-    const uint32_t slot = (h + (uint32_t)lane) & c.mask;
-    uint32_t f = 0u;
-    bool same = false;
-    if (lane < kProbe) {  // flag and key in one round trip (the key only counts when the flag is ready)
-        f = ld_agent(c.flag + slot);
-        same = key_is(c, slot, s);
-    }
-    const uint64_t hit = __ballot(lane < kProbe && flag_ready(f) && same);
+    const uint64_t h64 = state_hash64(s);
+    const uint32_t h = (uint32_t)h64, tag = state_tag(h64);
+    const uint32_t f = lane < kProbe ? ld_agent(c.flag + ((h + (uint32_t)lane) & c.mask)) : 0u;
+    const uint64_t cand = __ballot(lane < kProbe && flag_ready(f) && flag_tag(f) == tag);
     const uint64_t empty = __ballot(lane < kProbe && f == 0u);
-    if (!hit) return false;
-    const int hl = __builtin_ctzll(hit);
+    if (!cand) return false;
+    const int hl = __builtin_ctzll(cand);
     if (empty && __builtin_ctzll(empty) < hl) return false;
     const uint32_t hs = (h + (uint32_t)hl) & c.mask;
     const uint32_t f1 = (uint32_t)__builtin_amdgcn_readlane((int)f, hl);
     const rsrc_t r = rec_rsrc(c, hs);
-    floatx4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (lane < kRecLanes - 2) v = __builtin_bit_cast(floatx4_t, __builtin_amdgcn_raw_buffer_load_b128(r, kRecVal + 16 * lane, 0, kSc1));
-    // seqlock read side: the payload loads are served before the re-check is issued; any writer
+    u32x4_t piece = {0u, 0u, 0u, 0u};
+    if (lane < kRecLanes) piece = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, kSc1);
+    // seqlock read side: the record loads are served before the re-check is issued; any writer
     // that touched the record since the probe bumped the flag first (claim), so the re-check differs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t *kw = reinterpret_cast<const uint32_t *>(&s);
+    const int o = 4 * (lane & 1);
+    const bool key_ok = piece[0] == kw[o] && piece[1] == kw[o + 1] && piece[2] == kw[o + 2] && piece[3] == kw[o + 3];
+    if (__ballot(lane < 2 && !key_ok)) return false;
     bool ok = true;
     if (lane == 0) ok = ld_agent(c.flag + hs) == f1;
     if (!__shfl(ok, 0)) return false;
-    if (lane < kRecLanes - 2) *reinterpret_cast<floatx4_t *>(dst + 4 * lane) = v;
+    if (lane >= 2 && lane < kRecLanes) *reinterpret_cast<u32x4_t *>(dst + 4 * (lane - 2)) = piece;
     return true;
 }
 
 // Wave-level insert of (s -> 81 priors, value): lane l holds prior l in p0 and prior 64 + l in p1
 // (l < 17). Lane 0 claims a slot by CAS (flag -> odd); the record is stored as 23 16-byte sc1
-// pieces and drained (s_waitcnt vmcnt(0)) before the new version is published, so a reader on
-// any XCD that sees the flag sees the data. A concurrent insert of the same key may leave a
-// harmless duplicate. When all kProbe slots hold other positions, one of them (chosen by the
-// hash) is replaced. Entries are exact, so the table never needs clearing while the evaluator
-// is unchanged: it stays warm across moves.
+// pieces and drained (s_waitcnt vmcnt(0)) before the new flag is published, so a reader on
+// any XCD that sees the flag sees the data. A ready slot with this position's tag counts as this
+// position (no insert; a 16-bit collision only costs a missed entry), and a concurrent insert of
+// the same key may leave a harmless duplicate. When all kProbe slots hold other positions, one of
+// them (chosen by the hash) is replaced. Entries are exact, so the table never needs clearing
+// while the evaluator is unchanged: it stays warm across moves.
 __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v) {
     if (!c.flag) return;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
-    uint32_t pub = 2u;
-    // the kProbe slots' flags and keys in one round trip (lanes 0..kProbe-1), then lane 0 acts on
-    // the first slot that holds this position or is empty; a lost claim falls back to probing
-    // one slot after another from there
-    const uint32_t h = state_hash(s);
-    uint32_t f = 0u;
-    bool same = false;
-    if (lane < kProbe) {
-        const uint32_t sl = (h + (uint32_t)lane) & c.mask;
-        f = ld_agent(c.flag + sl);
-        same = key_is(c, sl, s);
-    }
-    const uint64_t here = __ballot(lane < kProbe && flag_ready(f) && same);
+    uint32_t pub = 0u;
+    // the kProbe slots' flags in one round trip (lanes 0..kProbe-1), then lane 0 acts on the first
+    // slot that holds this position's tag or is empty; a lost claim falls back to probing one slot
+    // after another from there
+    const uint64_t h64 = state_hash64(s);
+    const uint32_t h = (uint32_t)h64, tag = state_tag(h64);
+    const uint32_t f = lane < kProbe ? ld_agent(c.flag + ((h + (uint32_t)lane) & c.mask)) : 0u;
+    const uint64_t here = __ballot(lane < kProbe && flag_ready(f) && flag_tag(f) == tag);
     const uint64_t free_ = __ballot(lane < kProbe && f == 0u);
     const uint64_t either = here | free_;
     const int first = either ? __builtin_ctzll(either) : kProbe;
@@ -374,27 +371,32 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
         int i0 = first;
         if (!present && first < kProbe) {
             const uint32_t sl = (h + (uint32_t)first) & c.mask;
-            if (atomicCAS(c.flag + sl, 0u, 1u) == 0u) slot = (int)sl;
-            else i0 = first + 1;
+            if (atomicCAS(c.flag + sl, 0u, 1u) == 0u) {
+                slot = (int)sl;
+                pub = flag_publish(0u, tag);
+            } else {
+                i0 = first + 1;
+            }
         }
         for (int i = i0; slot < 0 && !present && i < kProbe; ++i) {
             const uint32_t sl = (h + (uint32_t)i) & c.mask;
-            const uint32_t f = ld_agent(c.flag + sl);
-            if (flag_ready(f) && key_is(c, sl, s)) {
+            const uint32_t fi = ld_agent(c.flag + sl);
+            if (flag_ready(fi) && flag_tag(fi) == tag) {
                 present = true;
                 break;
             }
-            if (f == 0u && atomicCAS(c.flag + sl, 0u, 1u) == 0u) {
+            if (fi == 0u && atomicCAS(c.flag + sl, 0u, 1u) == 0u) {
                 slot = (int)sl;
+                pub = flag_publish(0u, tag);
                 break;
             }
         }
-        if (slot < 0 && !present) {  // every probe slot taken: replace one (version f -> f + 1 -> f + 2)
+        if (slot < 0 && !present) {  // every probe slot taken: replace one (version v -> v + 1 -> v + 2)
             const uint32_t sl = (h + (h >> 29)) & c.mask;
-            const uint32_t f = ld_agent(c.flag + sl);
-            if (flag_ready(f) && atomicCAS(c.flag + sl, f, f + 1u) == f) {
+            const uint32_t fr = ld_agent(c.flag + sl);
+            if (flag_ready(fr) && atomicCAS(c.flag + sl, fr, fr + 1u) == fr) {
                 slot = (int)sl;
-                pub = flag_next(f);
+                pub = flag_publish(fr, tag);
                 atomicAdd(stripe_of(c.ctr + 3 * kRow), 1ull);
             }
         }
