@@ -122,9 +122,11 @@ class GraphedStep:
         side.wait_stream(torch.cuda.current_stream(dev))
         # MIOpen's immediate mode (heuristic kernel choice), whatever torch.backends.cudnn.benchmark
         # says (the reference's dual_network.py sets it at import): with find mode the captured step
-        # ran 7x slower and trained to a different loss (round 3, tools/bench_train.py). tune=True
-        # (round 4 experiment): MIOpen's find runs first in two eager steps outside any capture, and the
-        # warm-up and capture then reuse its choices (benchmark mode, results cached per shape)
+        # ran 7x slower and trained to a different loss (round 3, tools/bench_train.py), because find
+        # then ran inside the warm-up on the side stream. tune=True (round 4, train_network's default):
+        # MIOpen's find runs first, in two eager steps on the current stream outside any capture, and the
+        # warm-up and capture reuse its choices (benchmark mode, results cached per shape): graph fp32
+        # 13.0k -> 16.3k samples/s, the same losses (tools/bench_train.py, profiles/r4/train_bench.json)
         if tune:
             with torch.backends.cudnn.flags(enabled=True, benchmark=True, deterministic=False):
                 for _ in range(2):
@@ -198,7 +200,7 @@ def _use_graph(graph, device, world):
 
 
 def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, device=None, seed=0, lr=0.001,
-                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=False):
+                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=None):
     """Train `model` (a DualNetwork) on `history` in place; returns the per-epoch mean losses.
     In a torch.distributed job every rank calls this with the same history and seed.
     graph (default on for one GPU; UTTT_TRAIN_GRAPH=0 disables): replay the step as a HIP graph
@@ -210,6 +212,9 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
     if precision is None:
         import os
         precision = os.environ.get("UTTT_TRAIN_PRECISION", "fp32")
+    if tune is None:  # MIOpen find before the capture (round 4: graph fp32 13.0k -> 16.3k samples/s)
+        import os
+        tune = os.environ.get("UTTT_TRAIN_TUNE", "1") != "0"
     if _use_graph(graph, device, world):
         return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision, tune)
     if precision != "fp32":
