@@ -128,6 +128,8 @@ struct Trees {
     uttt_state_t *leaf;
     LeafRec *rec;
     int32_t *path;    // [tree][kMaxDepth]
+    uint4 *path_rec;  // [tree][kMaxDepth]: the path nodes' records as the select read them (k_apply's back-up
+                      // starts from them instead of re-reading each node: one dependent round trip less)
     int32_t *pending; // [tree]
     int32_t *tree_of; // [slot]
     int32_t *count;   // [0] pending leaves this round, [1] trees stopped by the select budget,
@@ -191,40 +193,64 @@ __device__ __forceinline__ void wave_argmax(float &v, int &i) {
     }
 }
 
-// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction), on one
-// 64-bit key per lane: the value's bits mapped to an order-preserving unsigned (-0 canonicalised to
-// +0, which compares equal to it; values are never NaN here: the per-lane scan's strict '>' from
-// -1e9 never takes one) above the complemented index, so "larger value, then smaller index" is the
-// unsigned order of the keys and each step is one compare and two selects, no branches. The order
-// is total, so any reduction tree gives the same winner: within each row of 16 lanes (quad swaps,
-// half-row and row mirrors), then row 0 into row 1 and row 2 into row 3 (row_bcast15), then row 1
-// into rows 2-3 (row_bcast31). The winner's index is valid in lane 63.
-__device__ __forceinline__ uint64_t argmax_key(float v, int i) {
-    uint32_t b = __float_as_uint(v + 0.0f);
-    b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-    return ((uint64_t)b << 32) | (uint64_t)(~(uint32_t)i);
-}
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void argmax_dpp(uint64_t &k) {
-    const int lo = (int)(uint32_t)k, hi = (int)(uint32_t)(k >> 32);
-    const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWS, 0xF, false);
-    const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWS, 0xF, false);
-    const uint64_t o = ((uint64_t)ohi << 32) | olo;
-    k = o > k ? o : k;
-}
-__device__ __forceinline__ int wave_argmax_to63(float v, int i) {
-    uint64_t k = argmax_key(v, i);
-    argmax_dpp<0xB1, 0xF>(k);   // quad_perm [1,0,3,2]
-    argmax_dpp<0x4E, 0xF>(k);   // quad_perm [2,3,0,1]
-    argmax_dpp<0x141, 0xF>(k);  // row_half_mirror
-    argmax_dpp<0x140, 0xF>(k);  // row_mirror
-    argmax_dpp<0x142, 0xA>(k);  // row_bcast15 -> rows 1, 3
-    argmax_dpp<0x143, 0xC>(k);  // row_bcast31 -> rows 2, 3
-    return (int)~(uint32_t)k;
-}
-
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction), in two
+// reductions of one instruction pair per step: the wave's largest value, then the smallest index among
+// the lanes holding it ("larger value, then smaller index": the reference's strict '>' scan in child
+// order). Values are never NaN here (the per-lane scan's strict '>' from -1e9 never takes one); -0 and
+// +0 compare equal, so they tie on the index as in the scan. Each reduction runs within each row of 16
+// lanes (quad swaps, half-row and row mirrors), then row 0 into row 1 and row 2 into row 3
+// (row_bcast15), then row 1 into rows 2-3 (row_bcast31): the result is valid in lane 63.
+// one reduction step as a single DPP-sourced VALU op (the two wait states a DPP read of a VGPR
+// written by the previous VALU op needs are in the asm: the compiler does not see inside it)
+#define UTTT_DPP_STEP(op, ctl)                                                                     \
+    __device__ __forceinline__ void op##_##ctl(uint32_t &k) {                                      \
+        asm volatile("s_nop 1\n\t" #op "_dpp %0, %0, %0 " UTTT_DPP_##ctl : "+v"(k));             \
+    }
+#define UTTT_DPP_q1 "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+#define UTTT_DPP_q2 "quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+#define UTTT_DPP_hm "row_half_mirror row_mask:0xf bank_mask:0xf"
+#define UTTT_DPP_rm "row_mirror row_mask:0xf bank_mask:0xf"
+#define UTTT_DPP_b15 "row_bcast:15 row_mask:0xa bank_mask:0xf"
+#define UTTT_DPP_b31 "row_bcast:31 row_mask:0xc bank_mask:0xf"
+UTTT_DPP_STEP(v_max_u32, q1)
+UTTT_DPP_STEP(v_max_u32, q2)
+UTTT_DPP_STEP(v_max_u32, hm)
+UTTT_DPP_STEP(v_max_u32, rm)
+UTTT_DPP_STEP(v_max_u32, b15)
+UTTT_DPP_STEP(v_max_u32, b31)
+UTTT_DPP_STEP(v_min_u32, q1)
+UTTT_DPP_STEP(v_min_u32, q2)
+UTTT_DPP_STEP(v_min_u32, hm)
+UTTT_DPP_STEP(v_min_u32, rm)
+UTTT_DPP_STEP(v_min_u32, b15)
+UTTT_DPP_STEP(v_min_u32, b31)
+__device__ __forceinline__ int wave_argmax_to63(float v, int i) {
+    // the value as an order-preserving unsigned (-0 canonicalised to +0 first), so each step of the max
+    // is an integer max (no float canonicalisation)
+    uint32_t b = __float_as_uint(v + 0.0f);
+    b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    uint32_t m = b;
+    v_max_u32_q1(m);   // quad_perm [1,0,3,2]
+    v_max_u32_q2(m);   // quad_perm [2,3,0,1]
+    v_max_u32_hm(m);   // row_half_mirror
+    v_max_u32_rm(m);   // row_mirror
+    v_max_u32_b15(m);  // row_bcast15 -> rows 1, 3
+    v_max_u32_b31(m);  // row_bcast31 -> rows 2, 3
+    asm volatile("s_nop 1");  // the asm's VALU write before the compiler's reads of m
+    const uint32_t top = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+    uint32_t k = b == top ? (uint32_t)i : (uint32_t)kNone;  // indices are >= 0: unsigned min is the int min
+    v_min_u32_q1(k);
+    v_min_u32_q2(k);
+    v_min_u32_hm(k);
+    v_min_u32_rm(k);
+    v_min_u32_b15(k);
+    v_min_u32_b31(k);
+    asm volatile("s_nop 1");
+    return (int)k;
 }
 
 // Orders this wave's global stores before its later global loads (other lanes
@@ -495,9 +521,10 @@ __device__ __forceinline__ float seq_sum_legal(float *row /* LDS, 16-B aligned, 
     return sum;
 }
 
-__device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi, int k,
-                              const uttt_state_t &s, float raw0, float raw1, float v, int &node_count,
-                              bool py = false, float *row = nullptr) {
+// rec_lo / rec_hi: this lane's path node's record (path[lane] / path[64 + lane]) as the select read it
+__device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi,
+                              uint4 rec_lo, uint4 rec_hi, int k, const uttt_state_t &s, float raw0, float raw1, float v,
+                              int &node_count, bool py = false, float *row = nullptr) {
     const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
@@ -537,8 +564,8 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     // children carry float64 priors when the policy summed to zero (kMetaP64)
     const uint32_t leaf_meta = (uint32_t)L << 23 | (py ? (kMetaWF32 | (p64 ? kMetaP64 : 0u)) : 0u);
     const uint32_t leaf_link = make_link((uint32_t)nb, (uint32_t)k);
-    auto update = [&](int pn, int d) {  // path node pn at depth d
-        uint4 r = pool.rec[base + pn];
+    auto update = [&](uint4 r, int pn, int d) {  // path node pn at depth d, its record r
+
         float w = __uint_as_float(r.x);
         const float x = ((depth - d) & 1) ? -v : v;
         for (int j = 0; j < k; ++j) w += x;
@@ -551,8 +578,8 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
         }
         pool.rec[base + pn] = r;
     };
-    if (lane <= depth) update(path_lo, lane);
-    if (lane + 64 <= depth) update(path_hi, lane + 64);
+    if (lane <= depth) update(rec_lo, path_lo, lane);
+    if (lane + 64 <= depth) update(rec_hi, path_hi, lane + 64);
     node_count = nb + blocks * L;
     return true;
 }
@@ -690,7 +717,7 @@ struct SelClock {
 // reference's strict '>' in child order.
 template <int NJ>
 __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int first, int c0, int cnt, float sq, int lane,
-                                           float &best, int &bi, uint2 &bl, SelClock &clk) {
+                                           float &best, int &bi, uint4 &bw, SelClock &clk) {
     uint4 r[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) r[j] = R[first + min(c0 + j * kWave + lane, cnt - 1)];
@@ -712,8 +739,10 @@ __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int firs
         const bool take = c < cnt && v[j] > best;
         best = take ? v[j] : best;
         bi = take ? c : bi;
-        bl.x = take ? r[j].z : bl.x;  // the winner's meta (visits, action, L) and link
-        bl.y = take ? r[j].w : bl.y;
+        bw.x = take ? r[j].x : bw.x;  // the winner's record: the back-ups start from it, its meta (visits,
+        bw.y = take ? r[j].y : bw.y;  // action, L) and link lead the descent on
+        bw.z = take ? r[j].z : bw.z;
+        bw.w = take ? r[j].w : bw.w;
     }
     clk.mark<kSpPuct>();
 }
@@ -748,6 +777,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             // the current node's meta (visits, action, L) and link (below the root: from the parent's scan)
             const uint4 r0 = R[0];
             uint2 nm = make_uint2(r0.z, r0.w);
+            // lane d: the record of path[d] (prec_lo) and path[64 + d] (prec_hi) as read on the way down
+            uint4 prec_lo = r0, prec_hi = make_uint4(0u, 0u, 0u, 0u);
             ++trips;
             clk.mark<kSpRoot>();
             bool fail = false;
@@ -758,10 +789,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 const int kself = (node == 0 && !PY) ? 0 : link_k(nm.y);
                 const int total = meta_n(nm.x) - kself;  // == sum of children's visits
                 int bi = kNone;
+                uint4 wr = make_uint4(0u, 0u, 0u, 0u);  // the chosen child's record
                 if (!PY) {
                     const float sq = sqrtf((float)total);
                     float best = -1e9f;
-                    uint2 bl = make_uint2(0u, 0u);
+                    uint4 bw = make_uint4(0u, 0u, 0u, 0u);
                     // Every load of a group of kScanGroup x 64 children is issued before the first
                     // compare (one memory round trip per group; a node expanded by a flush of k = 8
                     // copies has up to 8 x 81 children), and each child's link word and visits come
@@ -769,14 +801,17 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
                         ++trips;
-                        if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bl, clk);
-                        else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bl, clk);
+                        if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, clk);
+                        else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, clk);
                     }
                     bi = __builtin_amdgcn_readlane(wave_argmax_to63(best, bi), 63);
-                    if (bi != kNone) {  // the winner's lane holds its meta and link words
+                    if (bi != kNone) {  // the winner's lane holds its record
                         const int wl = bi & (kWave - 1);
-                        nm = make_uint2((uint32_t)__builtin_amdgcn_readlane((int)bl.x, wl),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)bl.y, wl));
+                        wr = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)bw.x, wl),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)bw.y, wl),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)bw.z, wl),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)bw.w, wl));
+                        nm = make_uint2(wr.z, wr.w);
                     }
                     clk.mark<kSpArgmax>();
                 } else {
@@ -825,13 +860,18 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     if (lane == 0) ctl.status |= kErrDepth;
                     break;
                 }
-                if (lane == (depth & 63)) {
-                    if (depth < 64) path_lo = node;
-                    else path_hi = node;
-                }
                 if (PY) {
-                    const uint4 rn = R[node];
-                    nm = make_uint2(rn.z, rn.w);
+                    wr = R[node];
+                    nm = make_uint2(wr.z, wr.w);
+                }
+                if (lane == (depth & 63)) {
+                    if (depth < 64) {
+                        path_lo = node;
+                        prec_lo = wr;
+                    } else {
+                        path_hi = node;
+                        prec_hi = wr;
+                    }
                 }
                 s = next_state(s, meta_action(nm.x));
                 clk.mark<kSpNext>();
@@ -845,14 +885,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
                 // backpropagate adds it at the leaf and flips sign upwards (:47-54).
                 const float v = -(lose ? -1.0f : 0.0f);
-                auto backup1 = [&](int pn, int d) {
-                    uint4 r = R[pn];
+                auto backup1 = [&](uint4 r, int pn, int d) {  // from the record read on the way down
                     r.x = __float_as_uint(__uint_as_float(r.x) + (((depth - d) & 1) ? -v : v));
                     r.z += 1u;
                     R[pn] = r;
                 };
-                if (lane <= depth) backup1(path_lo, lane);
-                if (lane + 64 <= depth) backup1(path_hi, lane + 64);
+                if (lane <= depth) backup1(prec_lo, path_lo, lane);
+                if (lane + 64 <= depth) backup1(prec_hi, path_hi, lane + 64);
                 wave_memory_fence();
                 trips += 2;
                 bytes += 16ull * (unsigned long long)(depth + 1);
@@ -876,8 +915,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 trips += 4;
                 // cv doubles as the prior sum's row: its values are in registers before the call
                 const float h0 = cv[lane], h1 = lane < 17 ? cv[64 + lane] : 0.0f, hv = cv[81];
-                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, k, s, h0, h1, hv, ctl.node_count, PY,
-                                   cv)) {
+                if (!expand_backup(pool, base, node, depth, path_lo, path_hi, prec_lo, prec_hi, k, s, h0, h1, hv,
+                                   ctl.node_count, PY, cv)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
                 }
@@ -896,8 +935,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             }
             if (cache.flag && lane == 0) atomicAdd(stripe_of(cache.ctr + kRow), 1ull);
             int32_t *gp = tr.path + (size_t)t * kMaxDepth;
-            if (lane <= depth) gp[lane] = path_lo;
-            if (lane + 64 <= depth) gp[lane + 64] = path_hi;
+            uint4 *gr = tr.path_rec + (size_t)t * kMaxDepth;
+            if (lane <= depth) {
+                gp[lane] = path_lo;
+                gr[lane] = prec_lo;
+            }
+            if (lane + 64 <= depth) {
+                gp[lane + 64] = path_hi;
+                gr[lane + 64] = prec_hi;
+            }
             if (lane == 0) {
                 LeafRec r;
                 r.node = node;
@@ -1051,6 +1097,8 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
     const size_t base = (size_t)t * pool.cap;
     const int32_t *gp = tr.path + (size_t)t * kMaxDepth;
     const int g_lo = gp[lane], g_hi = gp[lane + 64];
+    const uint4 *gr = tr.path_rec + (size_t)t * kMaxDepth;
+    const uint4 pr_lo = gr[lane], pr_hi = gr[lane + 64];  // the path nodes' records as the select read them
     float raw0 = 0.0f, raw1 = 0.0f, rawv = 0.0f;
     if (!per_copy) {
         const float *pol = policy + (int64_t)slot * pld;
@@ -1086,8 +1134,8 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             }
         }
         const bool cacheable = __ballot(!fin0 || (lane < 17 && !fin1)) == 0ull;
-        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f, v,
-                           ctl.node_count, tr.py != 0, s_row[threadIdx.x >> 6])) {
+        if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, pr_lo, pr_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f,
+                           v, ctl.node_count, tr.py != 0, s_row[threadIdx.x >> 6])) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
@@ -1128,8 +1176,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             }
             return;
         }
-        uint4 r_lo = lane <= depth ? pool.rec[base + pn_lo] : make_uint4(0u, 0u, 0u, 0u);
-        uint4 r_hi = lane + 64 <= depth ? pool.rec[base + pn_hi] : make_uint4(0u, 0u, 0u, 0u);
+        uint4 r_lo = pr_lo, r_hi = pr_hi;
         float w_lo = __uint_as_float(r_lo.x), w_hi = __uint_as_float(r_hi.x);
         for (int j = 0; j < k; ++j) {
             const int64_t row = (int64_t)rowbase[slot] + j;
@@ -1859,7 +1906,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     if ((rc = alloc_n(e, &e->pool.rec, nodes))) return fail(rc);
     if ((rc = alloc_n(e, &e->tr.ctl, max_trees)) || (rc = alloc_n(e, &e->tr.root, max_trees)) ||
         (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
-        (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
+        (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) ||
+        (rc = alloc_n(e, &e->tr.path_rec, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
         (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount * kRow)) ||
