@@ -154,6 +154,22 @@ def test_selfplay_matches_oracle_and_is_slot_invariant(gpu, oracle_lib):
             assert np.array_equal(r["values"], ref[g]["values"].astype(np.int64))
 
 
+@pytest.mark.parametrize("tau", [0.0, 0.5, 2.0])
+def test_selfplay_other_temperatures_match_oracle(gpu, oracle_lib, tau):
+    """k_move_end's one-hot (tau 0) and pow (tau != 1) score paths against the oracle's
+    boltzman (uttt_mcts.cpp:199-216) and self_play_cpp.play (:63-92)."""
+    n_games, seed = 6, 4242
+    ref = [oracle_lib.self_play_game_hash(seed + g, tau, 30, 4) for g in range(n_games)]
+    sp = gpu.SelfPlay(3, 30, 4, tau)
+    sp.run(0, n_games, seed)
+    recs = sp.records()
+    assert len(recs) == n_games
+    for g, r in enumerate(recs):
+        assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (tau, g)
+        assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64)), (tau, g)
+        assert np.array_equal(r["values"], ref[g]["values"].astype(np.int64))
+
+
 def test_play_uses_and_advances_global_numpy_rng(gpu):
     import self_play_cpp
     from oracle.hashnp import make_hash_model

@@ -130,8 +130,10 @@ struct Trees {
     int32_t *path;    // [tree][kMaxDepth]
     uint4 *path_rec;  // [tree][kMaxDepth]: the path nodes' records as the select read them (k_apply's back-up
                       // starts from them instead of re-reading each node: one dependent round trip less)
-    int32_t *pending; // [tree]
+    int32_t *pending; // [tree]: 0 nothing, 2 stopped by the select budget, 1 / 3 a queued leaf (3: the
+                      // tree has simulations left after it) | the leaf's depth << 8
     int32_t *tree_of; // [slot]
+    int32_t *depth_of; // [slot]: the queued leaf's depth (k_apply loads only the path entries it uses)
     int32_t *count;   // [0] pending leaves this round, [1] trees stopped by the select budget,
                       // [2] trees with simulations left after this round's apply
     int32_t n_trees;
@@ -376,9 +378,9 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
 // position (no insert; a 16-bit collision only costs a missed entry), and a concurrent insert of
 // the same key may leave a harmless duplicate. When all kProbe slots hold other positions, one of
 // them (chosen by the hash) is replaced. Entries are exact, so the table never needs clearing
-// while the evaluator is unchanged: it stays warm across moves.
-__device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v) {
-    if (!c.flag) return;
+// while the evaluator is unchanged: it stays warm across moves. Returns whether a record was written.
+__device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v) {
+    if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
     uint32_t pub = 0u;
@@ -428,7 +430,7 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
         }
     }
     slot = __shfl(slot, 0);
-    if (slot < 0) return;
+    if (slot < 0) return false;
     pub = (uint32_t)__builtin_amdgcn_readfirstlane((int)pub);
     // piece j of the record: j < 2 the key's words 4j..4j+3, else values 4(j-2)..4(j-2)+3
     // (value e < 64: lane e's p0; e < 81: lane e-64's p1; e == 81: v)
@@ -453,6 +455,7 @@ __device__ void cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
         st_agent(c.flag + slot, pub);
         atomicAdd(stripe_of(c.ctr + 2 * kRow), 1ull);
     }
+    return true;
 }
 
 // ---------------------------------------------------------- expand + backup --
@@ -758,6 +761,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     int pend = 0;
     unsigned long long bytes = 0;
     unsigned int levels = 0;
+    // cache hits / misses of this tree, counted once at the end: an atomic per hit made the next
+    // descent's first load wait for it (vmcnt counts the atomic), ~2k cycles a descent (round 4)
+    unsigned int hits = 0, misses = 0;
     // dependent round trips of this wave: the control loads, then per descent the root's link and visits,
     // one per child-scan group, and for a completion in place the cache probe, payload and re-check,
     // the path's read-modify-write and the fence
@@ -922,8 +928,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 }
                 clk.mark<kSpExpand>();
                 wave_memory_fence();
-                if (lane == 0) atomicAdd(stripe_of(cache.ctr), 1ull);
-                bytes += 20ull * (unsigned long long)(k * (int)legal_count(s)) + 16ull * (depth + 1);
+                ++hits;
+                // the probe's flags, the record, the k child blocks and the path's records
+                bytes += 32ull + 368ull + 16ull * (unsigned long long)(k * (int)legal_count(s)) + 16ull * (depth + 1);
                 clk.mark<kSpHitTail>();
                 sims_done += k;
                 if (sims_done >= tr.sims) break;
@@ -933,7 +940,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 }
                 continue;
             }
-            if (cache.flag && lane == 0) atomicAdd(stripe_of(cache.ctr + kRow), 1ull);
+            misses += cache.flag ? 1u : 0u;
             int32_t *gp = tr.path + (size_t)t * kMaxDepth;
             uint4 *gr = tr.path_rec + (size_t)t * kMaxDepth;
             if (lane <= depth) {
@@ -953,8 +960,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 tr.rec[t] = r;
                 tr.leaf[t] = s;
             }
+            // the probe's flags, the queued path (indices and records), LeafRec and state
+            bytes += (cache.flag ? 32ull : 0ull) + 20ull * (unsigned long long)(depth + 1) + 48ull;
             // 3: this leaf's k simulations leave the tree more to do (after its apply)
-            pend = sims_done + k < tr.sims ? 3 : 1;
+            pend = (sims_done + k < tr.sims ? 3 : 1) | depth << 8;
             clk.mark<kSpQueue>();
             break;
         }
@@ -964,6 +973,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     clk.flush(trips);
     if (lane == 0) {
         tr.pending[t] = pend;
+        if (hits) atomicAdd(stripe_of(cache.ctr), (unsigned long long)hits);
+        if (misses) atomicAdd(stripe_of(cache.ctr + kRow), (unsigned long long)misses);
         if (stats && bytes) atomicAdd(stripe_of(stats + kKSelect * kRow), bytes);
         if (stats && levels) {
             atomicAdd(stripe_of(stats + kKSelLevels * kRow), (unsigned long long)levels);
@@ -1034,7 +1045,7 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     const int b = tid * per, e = min(b + per, tr.n_trees);
     unsigned long long local = 0, cap = 0, mo = 0;
     for (int i = b; i < e; ++i) {
-        const int p = tr.pending[i];
+        const int p = tr.pending[i] & 0xFF;
         local += p == 1 || p == 3;
         cap += p == 2;
         mo += p >= 2;
@@ -1043,8 +1054,13 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     unsigned long long tot;
     const unsigned long long ex = block_scan_1024(local | (cap << 21) | (mo << 42), &tot, wsum);
     int slot = (int)(ex & 0x1FFFFFull);
-    for (int i = b; i < e; ++i)
-        if (tr.pending[i] == 1 || tr.pending[i] == 3) tr.tree_of[slot++] = i;
+    for (int i = b; i < e; ++i) {
+        const int p = tr.pending[i];
+        if ((p & 1) != 0) {  // 1 or 3
+            tr.depth_of[slot] = p >> 8;
+            tr.tree_of[slot++] = i;
+        }
+    }
     if (tid == 0) {
         tr.count[0] = (int)(tot & 0x1FFFFFull);
         tr.count[1] = (int)((tot >> 21) & 0x1FFFFFull);
@@ -1085,20 +1101,29 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
     __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];  // the prior sum's row, per wave
     const int lane = lane_id();
     const int slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    // two dependent round trips before the work: the count with this slot's tree (tree_of holds
-    // n_trees entries, stale past the count), then the tree's records, its path and the slot's
-    // evaluation, all loaded unconditionally (branch-free; masked where used)
+    // two dependent round trips before the work: the count with this slot's tree and leaf depth
+    // (tree_of / depth_of hold n_trees entries, stale past the count), then the tree's records, the
+    // path entries 0..depth (round 4: all 128 were loaded, 2.5 KB a leaf) and the slot's evaluation
     const int cnt = tr.count[0];
     const int t = tr.tree_of[slot < tr.n_trees ? slot : 0];
+    const int dq = tr.depth_of[slot < tr.n_trees ? slot : 0];
     if (slot >= cnt) return;
     const LeafRec r = tr.rec[t];
     TreeCtl ctl = tr.ctl[t];
     const uttt_state_t s = tr.leaf[t];
     const size_t base = (size_t)t * pool.cap;
     const int32_t *gp = tr.path + (size_t)t * kMaxDepth;
-    const int g_lo = gp[lane], g_hi = gp[lane + 64];
     const uint4 *gr = tr.path_rec + (size_t)t * kMaxDepth;
-    const uint4 pr_lo = gr[lane], pr_hi = gr[lane + 64];  // the path nodes' records as the select read them
+    int g_lo = 0, g_hi = 0;
+    uint4 pr_lo = {0u, 0u, 0u, 0u}, pr_hi = {0u, 0u, 0u, 0u};  // the path nodes' records as the select read them
+    if (lane <= dq) {
+        g_lo = gp[lane];
+        pr_lo = gr[lane];
+    }
+    if (lane + 64 <= dq) {
+        g_hi = gp[lane + 64];
+        pr_hi = gr[lane + 64];
+    }
     float raw0 = 0.0f, raw1 = 0.0f, rawv = 0.0f;
     if (!per_copy) {
         const float *pol = policy + (int64_t)slot * pld;
@@ -1111,6 +1136,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
     const int pn_lo = lane <= depth ? g_lo : 0;
     const int pn_hi = lane + 64 <= depth ? g_hi : 0;
     int L = 0;
+    bool inserted = false;
     const int nodes_before = ctl.node_count;
     if (!per_copy) {
         const float v = rawv;
@@ -1142,7 +1168,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             }
             return;
         }
-        if (cacheable) cache_insert(cache, s, raw0, raw1, v);
+        inserted = cacheable && cache_insert(cache, s, raw0, raw1, v);
         L = (ctl.node_count - nodes_before) / k;
     } else {
         // the reference's exact call pattern: k results, one per queued copy, applied in order
@@ -1214,9 +1240,14 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
         ctl.sims_done += k;
         tr.ctl[t] = ctl;
         if (bytes_ctr) {
+            // algorithmic bytes of one leaf: the slot's tree, depth and count (12), its LeafRec, TreeCtl and
+            // state (64), the path's indices and records (20 per level), the evaluation (328 per copy);
+            // written: the k child blocks (16 per child), the path's records (16 per level), the TreeCtl
+            // (16); with the evaluation cache: the probe's 8 flags (32) and a new record (368 + 4)
             const int copies = per_copy ? k : 1;
-            const unsigned long long b = 20ull * (unsigned long long)(k * L) + 81ull * 4ull * copies + 4ull * copies +
-                                         8ull + 16ull * (unsigned long long)(depth + 1);
+            const unsigned long long b = 12ull + 64ull + 36ull * (unsigned long long)(depth + 1) + 328ull * copies +
+                                         16ull * (unsigned long long)(k * L) + 16ull + (cache.flag ? 32ull : 0ull) +
+                                         (inserted ? 372ull : 0ull);
             atomicAdd(stripe_of(bytes_ctr), b);
         }
     }
@@ -1451,33 +1482,50 @@ __global__ __launch_bounds__(256) void k_tree_err(const TreeCtl *__restrict__ ct
     if (st & kErrMask) atomicMin(err, ((unsigned long long)s << 32) | st);
 }
 
-// One thread per slot: the per-move tail of self_play_cpp.play (:63-92). The slot's f64
-// policy-target row is worked on in LDS (one column of 81 doubles per thread, conflict-free:
-// the threads of a wave read one row), then stored to this ply's row in HBM once; worked on in
-// HBM, every read after a store was a dependent round trip.
-__global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const unsigned long long *err) {
-    __shared__ double s_pt[81][64];
+// A double held by lane i of the wave (i uniform), to every lane: the sequential f64 sums below run
+// the reference's additions in its order on values spread over the lanes, without an LDS round trip.
+__device__ __forceinline__ double lane_double(double x, int i) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), i);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ float lane_float(float x, int i) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), i));
+}
+// entry i of a row held as two halves (lane i: x0, lane i - 64: x1)
+__device__ __forceinline__ double row_entry(double x0, double x1, int i) {
+    return i < 64 ? lane_double(x0, i) : lane_double(x1, i - 64);
+}
+
+// One wave per slot: the per-move tail of self_play_cpp.play (:63-92). Entry i of the root's score
+// row lives in lane i (x0) and lane i - 64 (x1); what is order-free (the arg-max, the f32 sum of
+// integer visit counts) is a wave reduction, what is not (np.sum's pairwise blocks, the cumsum of
+// np.random.choice) runs the reference's additions in its order on readlane operands, the same in
+// every lane. Round 3's thread-per-slot form walked the row in LDS, 81-step dependent chains per pass.
+__global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, const unsigned long long *err) {
     // asynchronous form: k_tree_err has folded the failed trees into *err; on a failure this move's
     // end changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
     if (err && *err != ~0ull) return;
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    // np.random.choice's random_sample (numpy legacy: two 32-bit draws, 53-bit double), drawn first by
-    // every live slot with the whole wave present: a key that runs out is twisted by all 64 lanes
-    // (mt_twist_wave), one key after another, instead of by its own thread
-    const bool in = s < sp.slots;
-    const bool draws = in && sp.slot[s].live;
-    uint32_t *key = sp.mt_key + (size_t)(in ? s : 0) * 624;
-    int32_t pos = draws ? sp.mt_pos[s] : 0;
-    uint32_t w1 = 0u, w2 = 0u;
-    if (draws && pos <= 623) w1 = mt_temper(key[pos]);
-    if (draws && pos <= 622) w2 = mt_temper(key[pos + 1]);
-    const bool tw = draws && pos >= 623;
-    for (uint64_t m = __ballot(tw); m; m &= m - 1ull) {
-        const int l = __builtin_ctzll(m);
-        mt_twist_wave(sp.mt_key + (size_t)(blockIdx.x * blockDim.x + l) * 624);
+    const int lane = lane_id();
+    const int s = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (s >= sp.slots) return;
+    Slot sl = sp.slot[s];
+    sl.finished = 0;
+    if (!sl.live) {
+        if (lane == 0) sp.slot[s] = sl;
+        return;
     }
-    if (tw) {
+    // np.random.choice's random_sample (numpy legacy: two 32-bit draws, 53-bit double); a key that
+    // runs out is twisted by the wave (mt_twist_wave)
+    uint32_t *key = sp.mt_key + (size_t)s * 624;
+    int32_t pos = sp.mt_pos[s];
+    uint32_t w1, w2;
+    if (pos >= 623) {
+        const uint32_t k623 = key[623];
+        mt_twist_wave(key);
         if (pos == 623) {  // the first word was key[623] before the twist
+            w1 = mt_temper(k623);
             w2 = mt_temper(key[0]);
             pos = 1;
         } else {
@@ -1486,97 +1534,120 @@ __global__ __launch_bounds__(64) void k_move_end(Pool pool, SelfPlay sp, const u
             pos = 2;
         }
     } else {
+        w1 = mt_temper(key[pos]);
+        w2 = mt_temper(key[pos + 1]);
         pos += 2;
     }
-    if (draws) sp.mt_pos[s] = pos;
     const double u = ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
-    if (!in) return;
-    Slot sl = sp.slot[s];
-    sl.finished = 0;
-    if (!sl.live) {
-        sp.slot[s] = sl;
-        return;
-    }
     const size_t base = (size_t)s * pool.cap;
     const int ply = sl.ply;
-    double *const pt = &s_pt[0][threadIdx.x];  // pt[i * 64]: element i of this slot's row
-    // root scores (uttt_mcts.cpp:177-192, as root_scores) as f32 values held exactly in pt[0..L)
+    // root visit counts (uttt_mcts.cpp:177-192, as root_scores): entry i in lane i / i - 64
     int first;
     const int L = root_children(pool, base, first);
+    const bool h0 = lane < L, h1 = lane + 64 < L;
+    const int n0 = h0 ? visits_of(pool, base + first + lane) : 0;
+    const int n1 = h1 ? visits_of(pool, base + first + lane + 64) : 0;
+    double x0, x1;
     if (sp.temperature == 0.0f) {
-        int mi = 0;
-        float mv = L ? (float)visits_of(pool, base + first) : 0.0f;
-        for (int i = 1; i < L; ++i) {
-            const float v = (float)visits_of(pool, base + first + i);
-            if (v > mv) {
-                mv = v;
-                mi = i;
-            }
-        }
-        for (int i = 0; i < L; ++i) pt[(i) * 64] = (i == mi) ? 1.0 : 0.0;
+        // one-hot first max: the largest count, then the lowest index holding it (counts < 2^24, so
+        // the f32 compares of the reference order them as the integers do)
+        int kk = max(h0 ? (n0 << 8) | (255 - lane) : -1, h1 ? (n1 << 8) | (255 - 64 - lane) : -1);
+#pragma unroll
+        for (int o = 32; o; o >>= 1) kk = max(kk, __shfl_xor(kk, o));
+        const int mi = kk < 0 ? 0 : 255 - (kk & 0xFF);
+        x0 = (h0 && lane == mi) ? 1.0 : 0.0;
+        x1 = (h1 && lane + 64 == mi) ? 1.0 : 0.0;
     } else {
         const double y = (double)(1.0f / sp.temperature);  // glibc powf: double pow, one rounding
-        float sum = 0.0f;
-        for (int i = 0; i < L; ++i) {
-            // pow(x, 1) == x exactly (IEEE 754): the self-play temperature 1.0 skips the call
-            const double xn = (double)visits_of(pool, base + first + i);
-            const float v = (float)(y == 1.0 ? xn : pow(xn, y));
-            pt[(i) * 64] = (double)v;
-            sum += v;
+        float v0 = 0.0f, v1 = 0.0f, sum = 0.0f;
+        if (y == 1.0) {
+            // pow(x, 1) == x exactly (IEEE 754); a sum of integers below 2^24 is exact in f32 in
+            // any order, so the reference's sequential sum is the wave's integer sum
+            v0 = (float)n0;
+            v1 = (float)n1;
+            int t = n0 + n1;
+#pragma unroll
+            for (int o = 32; o; o >>= 1) t += __shfl_xor(t, o);
+            sum = (float)t;
+        } else {
+            if (h0) v0 = (float)pow((double)n0, y);
+            if (h1) v1 = (float)pow((double)n1, y);
+            for (int i = 0; i < L; ++i) sum += i < 64 ? lane_float(v0, i) : lane_float(v1, i - 64);
         }
-        if (sum > 0)
-            for (int i = 0; i < L; ++i) pt[(i) * 64] = (double)((float)pt[(i) * 64] / sum);
+        if (sum > 0) {
+            v0 = v0 / sum;
+            v1 = v1 / sum;
+        }
+        x0 = (double)v0;
+        x1 = (double)v1;
     }
-    // scores -> float64, renormalised with np.sum (:74-78)
-    const double tot = np_sum(pt, L, 64);
-    for (int i = 0; i < L; ++i) pt[(i) * 64] = (tot == 0.0) ? 1.0 / (double)L : pt[(i) * 64] / tot;
-    // policy target (:81-83): entry i moves to its action (the i-th legal action >= i, so a
-    // descending scatter never overwrites an entry it still has to move), the rest are zero
+    // scores -> float64, renormalised with np.sum (:74-78): np.add.reduce's pairwise block (8
+    // accumulators over i = j mod 8, then the remainder), the same additions in every lane
+    double tot;
+    if (L < 8) {
+        tot = 0.0;
+        for (int i = 0; i < L; ++i) tot += row_entry(x0, x1, i);
+    } else {
+        double r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = lane_double(x0, j);
+        int i = 8;
+        for (; i < L - (L % 8); i += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] += row_entry(x0, x1, i + j);
+        tot = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < L; ++i) tot += row_entry(x0, x1, i);
+    }
+    x0 = h0 ? ((tot == 0.0) ? 1.0 / (double)L : x0 / tot) : 0.0;
+    x1 = h1 ? ((tot == 0.0) ? 1.0 / (double)L : x1 / tot) : 0.0;
+    // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right. The
+    // cumsum's prefixes land in the lanes of their entries; its last prefix is cdf[-1].
+    double c0 = 0.0, c1 = 0.0, acc = 0.0;
+    for (int i = 0; i < L; ++i) {
+        acc += row_entry(x0, x1, i);
+        if (lane == (i & 63)) {
+            if (i < 64) c0 = acc;
+            else c1 = acc;
+        }
+    }
+    const uint64_t b0 = __ballot(h0 && !(c0 / acc <= u)), b1 = __ballot(h1 && !(c1 / acc <= u));
+    const int k = b0 ? __builtin_ctzll(b0) : (b1 ? 64 + __builtin_ctzll(b1) : L - 1);  // idx >= L -> L - 1
+    // policy target (:81-83): entry i of the row goes to the i-th legal action, the rest are zero
     uint32_t m[3];
     legal_mask(sl.state, m);
-    {
-        int i = L - 1;
-        for (int w = 2; w >= 0; --w)
-            for (int b = 26; b >= 0; --b)
-                if ((m[w] >> b) & 1u) {
-                    pt[(27 * w + b) * 64] = pt[(i) * 64];
-                    --i;
-                }
-        for (int a = 0; a < 81; ++a)
-            if (!((m[a / 27] >> (a % 27)) & 1u)) pt[(a) * 64] = 0.0;
-    }
-    // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right.
-    // Two passes over the legal actions in order, the same additions in the same order.
-    double last = 0.0;
-    for (int w = 0; w < 3; ++w)
-        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) last += pt[(27 * w + __builtin_ctz(bits)) * 64];
-    int action = -1, final_action = -1;
-    double acc = 0.0;
-    for (int w = 0; w < 3 && action < 0; ++w)
-        for (uint32_t bits = m[w]; bits; bits &= bits - 1u) {
-            const int a = 27 * w + __builtin_ctz(bits);
-            acc += pt[(a) * 64];
-            final_action = a;
-            if (!(acc / last <= u)) {
-                action = a;
-                break;
-            }
-        }
-    if (action < 0) action = final_action;  // idx >= L -> L - 1
     double *const row = sp.ply_policy + ((size_t)s * kMaxPlies + ply) * 81;
-    for (int a = 0; a < 81; ++a) row[a] = pt[a * 64];
-    sp.ply_state[(size_t)s * kMaxPlies + ply] = sl.state;
-    sp.ply_action[(size_t)s * kMaxPlies + ply] = (int8_t)action;
-    sl.state = next_state(sl.state, action);
-    sl.ply = ply + 1;
-    if (is_done(sl.state) || sl.ply >= kMaxPlies) {
-        sl.finished = 1;
-        sl.fin_len = sl.ply;
-        sl.fin_game = sl.game;
-        sl.fin_value = is_lose(sl.state) ? -1 : 0;  // self_play_cpp.py:95
-        sl.live = 0;
+    int action = -1;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const int a = lane + 64 * half;
+        int rank = 0;
+        bool legal = false;
+        if (a < 81) {
+            const int w = a / 27, b = a % 27;
+            legal = (m[w] >> b) & 1u;
+            rank = __builtin_popcount(m[w] & ((1u << b) - 1u));
+            for (int q = 0; q < w; ++q) rank += __builtin_popcount(m[q]);
+        }
+        const double e0 = __shfl(x0, rank & 63), e1 = __shfl(x1, rank & 63);
+        if (a < 81) row[a] = legal ? (rank < 64 ? e0 : e1) : 0.0;
+        const uint64_t hit = __ballot(legal && rank == k);
+        if (hit) action = 64 * half + __builtin_ctzll(hit);
     }
-    sp.slot[s] = sl;
+    if (lane == 0) {
+        sp.mt_pos[s] = pos;
+        sp.ply_state[(size_t)s * kMaxPlies + ply] = sl.state;
+        sp.ply_action[(size_t)s * kMaxPlies + ply] = (int8_t)action;
+        sl.state = next_state(sl.state, action);
+        sl.ply = ply + 1;
+        if (is_done(sl.state) || sl.ply >= kMaxPlies) {
+            sl.finished = 1;
+            sl.fin_len = sl.ply;
+            sl.fin_game = sl.game;
+            sl.fin_value = is_lose(sl.state) ? -1 : 0;  // self_play_cpp.py:95
+            sl.live = 0;
+        }
+        sp.slot[s] = sl;
+    }
 }
 
 // One block: give finished games arena rows (slot order) and free slots the
@@ -1908,7 +1979,7 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) ||
         (rc = alloc_n(e, &e->tr.path_rec, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
-        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
+        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.depth_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount * kRow)) ||
         (rc = alloc_n(e, &e->d_cache_ctr, 4 * kRow)))
@@ -2355,7 +2426,7 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
     {
         TimedLaunch tl(e, kKMoveEnd);
         const unsigned long long *no_err = nullptr;
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp, no_err);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, no_err);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, no_err);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, no_err);
     }
@@ -2421,7 +2492,7 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
         hipLaunchKernelGGL(k_tree_err, dim3((slots + 255) / 256), dim3(256), 0, e->stream, (const TreeCtl *)e->tr.ctl,
                            slots, e->d_err);
         const unsigned long long *err = e->d_err;
-        hipLaunchKernelGGL(k_move_end, dim3((slots + 63) / 64), dim3(64), 0, e->stream, e->pool, e->sp, err);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, err);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, err);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, err);
     }
