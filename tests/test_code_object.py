@@ -27,7 +27,7 @@ PRODUCT = {
 }
 
 
-def kernel_metadata(tmp_path):
+def code_objects(tmp_path):
     fb = tmp_path / "fatbin.bin"
     subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fb}", LIB], check=True, capture_output=True)
     # one offload bundle per linked source file (engine, nn_kernels, wino3h_conv), concatenated
@@ -44,6 +44,11 @@ def kernel_metadata(tmp_path):
                        check=True, capture_output=True)
         notes += subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], check=True, capture_output=True,
                                 text=True).stdout
+    return notes, [tmp_path / f"gfx950_{i}.o" for i in range(len(starts))]
+
+
+def kernel_metadata(tmp_path):
+    notes, _ = code_objects(tmp_path)
     meta = {}
     # one YAML map per kernel in amdhsa.kernels; its keys are sorted, .name before .private_segment_fixed_size
     for block in re.split(r"\n\s+- \.", notes):
@@ -63,3 +68,37 @@ def test_product_kernels_use_no_scratch(tmp_path):
         assert hits, f"{label} not found in the code object"
         for k, v in hits.items():
             assert v == 0, f"{label} ({k}) uses {v} bytes of scratch (register spills)"
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf")),
+                    reason="library not built or ROCm LLVM tools missing")
+def test_tree_kernels_do_not_read_the_dispatch_packet(tmp_path):
+    """k_select / k_apply must not set ENABLE_SGPR_DISPATCH_PTR (kernel descriptor, kernel_code_properties
+    bit 1): the compiler asks for the dispatch packet when it places a private array in LDS addressed by
+    the flat work-item id, and that read (the AQL packet, host memory) cost 2-26 us at the start of every
+    k_select launch in round 4 ("What a k_select launch waits for")."""
+    import struct
+    _, objs = code_objects(tmp_path)
+    checked = set()
+    for co in objs:
+        elf = co.read_bytes()
+        shoff, = struct.unpack_from("<Q", elf, 0x28)
+        shentsize, shnum = struct.unpack_from("<HH", elf, 0x3A)
+        secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+        for sec in secs:
+            if sec[1] != 2:  # SHT_SYMTAB
+                continue
+            strtab = secs[sec[6]]
+            for j in range(sec[5] // 24):
+                st_name, _, _, st_shndx, st_value, _ = struct.unpack_from("<IBBHQQ", elf, sec[4] + 24 * j)
+                end = elf.index(b"\0", strtab[4] + st_name)
+                name = elf[strtab[4] + st_name:end].decode()
+                if not name.endswith(".kd") or not any(
+                        frag in name for frag in ("8k_selectILb0E", "8k_selectILb1E", "7k_applyE")):
+                    continue
+                tgt = secs[st_shndx]
+                kd = elf[tgt[4] + st_value - tgt[3]:][:64]
+                props, = struct.unpack_from("<H", kd, 56)
+                assert not (props & 0x2), f"{name} reads the dispatch packet (kernel_code_properties {props:#x})"
+                checked.add(name)
+    assert len(checked) >= 3, checked

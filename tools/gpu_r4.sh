@@ -41,6 +41,9 @@ for s in $STEPS; do
                -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \
                > $OUT/tprof.log 2>&1 ;;
     selcyc) timeout -k 10 300 python -u tools/diag/select_cycles.py ${SELCYC_ARGS:-} > $OUT/select_cycles.log 2>&1 ;;
+    pretouch) for m in 0 1 2 3; do  # k_select's first root load: TLB or line? (engine.hip g_sel_pretouch)
+                timeout -k 10 300 python -u tools/diag/select_cycles.py 100 10 $m > $OUT/pretouch_$m.log 2>&1 || exit $?
+              done ;;
     stamps) timeout -k 10 300 python -u tools/diag/wino3h_stamps.py 1344 16384 > $OUT/stamps.log 2>&1 ;;
     lat)   timeout -k 10 300 python -u tools/diag/latency_single.py > $OUT/latency.log 2>&1 ;;
     vsmall) VARIANTS= timeout -k 10 300 python -u tools/diag/wino3h_variants.py 250 500 1000 > $OUT/variants_small.log 2>&1 ;;
@@ -64,9 +67,9 @@ for s in $STEPS; do
            for i in 1 2; do
              for lib in base new; do
                envs=""; [ $lib = base ] && envs="UTTT_ENGINE_LIB=$PWD/ultimate-tictactoe-alphazero_amd/libuttt_engine_base.so"
-               for ev in fused hash; do
+               for ev in ${ABL_EVS:-fused hash}; do
                  env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps ${AB_STEPS:-10} --warmup 4 \
-                   --evaluator $ev > $OUT/abl_${lib}_${ev}_$i.log 2>&1 || exit $?
+                   --evaluator $ev ${ABL_ARGS:-} > $OUT/abl_${lib}_${ev}_$i.log 2>&1 || exit $?
                  echo "$lib $ev $i $(tail -1 $OUT/abl_${lib}_${ev}_$i.log | cut -c1-200)" >> $OUT/abl.log
                done
              done

@@ -307,6 +307,15 @@ __device__ __forceinline__ uint64_t state_hash64(const uttt_state_t &s) {
 // a position's tag: the top 16 bits of its hash (its slot: the low 32 bits)
 __device__ __forceinline__ uint32_t state_tag(uint64_t h64) { return (uint32_t)(h64 >> 48); }
 
+// 16-byte piece `hi` (0 or 1) of a position's 32-byte key, by selects: indexing the state's words by a
+// lane-dependent offset made the state a private array, which the compiler placed in LDS addressed by
+// the flat work-item id, i.e. a read of the dispatch packet in host memory at every launch (round 4:
+// 2-26 us before k_select's first descent, tools/diag/select_cycles.py)
+__device__ __forceinline__ uint4 key_piece(const uttt_state_t &s, bool hi) {
+    return make_uint4(hi ? s.opp[1] : s.own[0], hi ? s.opp[2] : s.own[1], hi ? s.mains : s.own[2],
+                      hi ? (uint32_t)s.active : s.opp[0]);
+}
+
 __device__ __forceinline__ bool same_state(const uttt_state_t &x, const uttt_state_t &y) {
     return x.own[0] == y.own[0] && x.own[1] == y.own[1] && x.own[2] == y.own[2] && x.opp[0] == y.opp[0] &&
            x.opp[1] == y.opp[1] && x.opp[2] == y.opp[2] && x.mains == y.mains && x.active == y.active;
@@ -360,9 +369,8 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
     // seqlock read side: the record loads are served before the re-check is issued; any writer
     // that touched the record since the probe bumped the flag first (claim), so the re-check differs
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t *kw = reinterpret_cast<const uint32_t *>(&s);
-    const int o = 4 * (lane & 1);
-    const bool key_ok = piece[0] == kw[o] && piece[1] == kw[o + 1] && piece[2] == kw[o + 2] && piece[3] == kw[o + 3];
+    const uint4 kp = key_piece(s, (lane & 1) != 0);
+    const bool key_ok = piece[0] == kp.x && piece[1] == kp.y && piece[2] == kp.z && piece[3] == kp.w;
     if (__ballot(lane < 2 && !key_ok)) return false;
     bool ok = true;
     if (lane == 0) ok = ld_agent(c.flag + hs) == f1;
@@ -442,11 +450,9 @@ __device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
         const float b = __shfl(p1, (e - 64) & 63);
         piece[i] = e < 64 ? a : (e < 81 ? b : (e == 81 ? v : 0.0f));
     }
-    const uint32_t *kw = reinterpret_cast<const uint32_t *>(&s);
     if (lane < 2) {
-        const int o = 4 * lane;
-        piece = floatx4_t{__uint_as_float(kw[o]), __uint_as_float(kw[o + 1]), __uint_as_float(kw[o + 2]),
-                          __uint_as_float(kw[o + 3])};
+        const uint4 kp = key_piece(s, lane != 0);
+        piece = floatx4_t{__uint_as_float(kp.x), __uint_as_float(kp.y), __uint_as_float(kp.z), __uint_as_float(kp.w)};
     }
     const rsrc_t r = rec_rsrc(c, (uint32_t)slot);
     if (lane < kRecLanes) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, piece), r, 16 * lane, 0, kSc1);
@@ -663,6 +669,7 @@ enum SelPhase {
     kSpExpand,      // expand + backup of a cache hit (prior sum, child blocks, path)
     kSpHitTail,     // fence + counters after a hit
     kSpQueue,       // pending-leaf record
+    kSpRootState,   // the tree's root state (once per launch, before the first descent)
     kSpCount
 };
 #ifdef UTTT_DIAG_BUILD
@@ -672,24 +679,41 @@ constexpr int kSelHeavyTrips = 24;
 // [heavy launches' phases][launches, heavy launches]
 constexpr int kSelDiagTrees = 8192;
 __device__ unsigned long long g_sel_cyc[kSelDiagTrees][2 * kSpCount + 2];
+// the last launch's wall-clock stamps per tree (s_memrealtime, a chip-wide 100 MHz counter): the wave's
+// start (its control loads served), its first root phase done, its end; trips in the launch
+__device__ unsigned long long g_sel_rt[kSelDiagTrees][4];
+// what a live tree's wave loads (and waits for) before its clock starts: 0 nothing, 1 the record 8 past
+// its root (another 128-B line of the same page), 2 its root record itself, 3 the record half a pool away
+__device__ int g_sel_pretouch;
+// the phase sums live in LDS (one row per wave): kept in registers they made k_select spill to
+// scratch, whose first accesses are what the diagnostics then measured
+__shared__ unsigned long long s_selclk[kWavesPerBlock][kSpCount];
 struct SelClock {
-    unsigned long long t, acc[kSpCount];
+    unsigned long long t, rt0, rt1;
+    unsigned long long *acc;
     __device__ __forceinline__ void start() {
+        acc = s_selclk[threadIdx.x >> 6];
+        if ((threadIdx.x & 63) < kSpCount) acc[threadIdx.x & 63] = 0ull;
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         t = __builtin_amdgcn_s_memtime();
-#pragma unroll
-        for (int i = 0; i < kSpCount; ++i) acc[i] = 0ull;
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        rt1 = 0ull;
     }
     template <int P>
     __device__ __forceinline__ void mark() {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const unsigned long long n = __builtin_amdgcn_s_memtime();
-        acc[P] += n - t;
+        if (P == kSpRoot && rt1 == 0ull) rt1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) acc[P] += n - t;
         t = n;
     }
     __device__ __forceinline__ void flush(unsigned int trips) {
         const int tree = (int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
         if ((threadIdx.x & 63) != 0 || tree >= kSelDiagTrees) return;
+        g_sel_rt[tree][0] = rt0;
+        g_sel_rt[tree][1] = rt1;
+        g_sel_rt[tree][2] = __builtin_amdgcn_s_memrealtime();
+        g_sel_rt[tree][3] = trips;
         unsigned long long *row = g_sel_cyc[tree];
         const int h = trips >= (unsigned int)kSelHeavyTrips;
 #pragma unroll
@@ -769,11 +793,20 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
     // the path's read-modify-write and the fence
     unsigned int trips = 1;
     SelClock clk;
+#ifdef UTTT_DIAG_BUILD
+    if (g_sel_pretouch && (ctl.status & kLive)) {
+        const uint4 *pr = pool.rec + (size_t)t * pool.cap;
+        const int off = g_sel_pretouch == 1 ? 8 : (g_sel_pretouch == 2 ? 0 : (int)(pool.cap / 2));
+        const uint32_t q = pr[off].x;
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(q) : "memory");
+    }
+#endif
     clk.start();
     if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
         const size_t base = (size_t)t * pool.cap;
         uint4 *__restrict__ R = pool.rec + base;
         const uttt_state_t root = tr.root[t];
+        clk.mark<kSpRootState>();
         int sims_done = ctl.sims_done;
         int budget = kSelectBudget;
         for (;;) {
@@ -2691,6 +2724,21 @@ int uttt_engine_kernel_stats(uttt_engine_t *e, int32_t kernel, double *total_ms,
 #ifdef UTTT_DIAG_BUILD
 // Diagnostics engine build only: k_select's phase cycles (SelClock) summed over the first kSelDiagTrees
 // trees, out[2 * kSpCount + 2]; reset zeroes them.
+// the last k_select launch's per-tree wall-clock stamps (g_sel_rt): out[tree * 4 + {start, first root
+// done, end, trips}], n_trees entries
+int uttt_diag_select_pretouch(int32_t mode) {
+    if (mode < 0 || mode > 3) return UTTT_ERR_ARG;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sel_pretouch), &mode, sizeof(mode)) == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
+}
+
+int uttt_diag_select_rt(unsigned long long *out, int32_t n_trees) {
+    static unsigned long long host[kSelDiagTrees][4];
+    if (!out || n_trees < 0 || n_trees > kSelDiagTrees) return UTTT_ERR_ARG;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sel_rt), sizeof(host)) != hipSuccess) return UTTT_ERR_HIP;
+    memcpy(out, host, sizeof(unsigned long long) * 4 * (size_t)n_trees);
+    return UTTT_OK;
+}
+
 int uttt_diag_select_cycles(unsigned long long *out, int32_t reset) {
     static unsigned long long host[kSelDiagTrees][2 * kSpCount + 2];
     if (out) {
