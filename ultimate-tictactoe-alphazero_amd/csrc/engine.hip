@@ -163,6 +163,12 @@ __device__ __forceinline__ uint4 new_child(float p, uint32_t action) {
 
 // ------------------------------------------------------------ wave helpers --
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+// This wave's global index (one wave per tree / slot / row), marked wave-uniform: what is derived from
+// it (the tree's control words, its states, the rules applied to them) lives in scalar registers and
+// runs on the scalar unit instead of as 64 identical vector lanes (round 4)
+__device__ __forceinline__ int wave_index() {
+    return __builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+}
 
 __device__ __forceinline__ uint64_t lanes_below() {
     const int l = lane_id();
@@ -779,7 +785,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                                                    unsigned long long *stats) {
     __shared__ __attribute__((aligned(16))) float s_hit[kWavesPerBlock][84];  // a cache hit's values, per wave
     const int lane = lane_id();
-    const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int t = wave_index();
     if (t >= tr.n_trees) return;
     TreeCtl ctl = tr.ctl[t];
     int pend = 0;
@@ -1133,7 +1139,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
                                                   unsigned long long *bytes_ctr) {
     __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];  // the prior sum's row, per wave
     const int lane = lane_id();
-    const int slot = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int slot = wave_index();
     // two dependent round trips before the work: the count with this slot's tree and leaf depth
     // (tree_of / depth_of hold n_trees entries, stale past the count), then the tree's records, the
     // path entries 0..depth (round 4: all 128 were loaded, 2.5 KB a leaf) and the slot's evaluation
@@ -1292,7 +1298,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
 __global__ __launch_bounds__(kBlock) void k_hash_eval(const float *__restrict__ x, int n, float *__restrict__ policy,
                                                       float *__restrict__ value) {
     const int lane = lane_id();
-    const int row = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int row = wave_index();
     if (row >= n) return;
     const float *xr = x + (size_t)row * 243;
     uint64_t w[4];
@@ -1353,7 +1359,7 @@ __device__ void root_scores(const Pool &pool, size_t base, float temperature, fl
 __global__ __launch_bounds__(kBlock) void k_hash_leaves(Trees tr, float *__restrict__ policy,
                                                         float *__restrict__ value) {
     const int lane = lane_id();
-    const int row = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int row = wave_index();
     if (row >= tr.count[0]) return;
     const uttt_state_t s = tr.leaf[tr.tree_of[row]];
     uint32_t m[3];
@@ -1541,7 +1547,7 @@ __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, con
     // end changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
     if (err && *err != ~0ull) return;
     const int lane = lane_id();
-    const int s = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int s = wave_index();
     if (s >= sp.slots) return;
     Slot sl = sp.slot[s];
     sl.finished = 0;
