@@ -140,6 +140,7 @@ struct Trees {
     int32_t sims;
     int32_t batch;
     int32_t py;  // 1: pv_mcts.py semantics (arena), 0: cpp/uttt_mcts.cpp (self-play)
+    int32_t budget;  // in-place completions per tree and select launch (kSelectBudget; UTTT_SELECT_BUDGET)
 };
 
 // record packing (Pool)
@@ -393,7 +394,12 @@ __device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *d
 // the same key may leave a harmless duplicate. When all kProbe slots hold other positions, one of
 // them (chosen by the hash) is replaced. Entries are exact, so the table never needs clearing
 // while the evaluator is unchanged: it stays warm across moves. Returns whether a record was written.
-__device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v) {
+// sum >= 0 marks `psum` (the sequential f32 sum of the legal priors, uttt_mcts.cpp:150-153, as
+// expand_backup computed it) valid: it is stored beside the values (value 82, with 1.0f at 83), so a
+// hit expands without re-adding up to 81 priors one dependent add after another.
+constexpr int kRecSum = 82, kRecSumFlag = 83;
+__device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v, bool has_sum = false,
+                             float psum = 0.0f) {
     if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
@@ -454,7 +460,9 @@ __device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
         const int e = 4 * (lane - 2) + i;
         const float a = __shfl(p0, e & 63);
         const float b = __shfl(p1, (e - 64) & 63);
-        piece[i] = e < 64 ? a : (e < 81 ? b : (e == 81 ? v : 0.0f));
+        piece[i] = e < 64 ? a
+                          : (e < 81 ? b
+                                    : (e == 81 ? v : (e == kRecSum && has_sum ? psum : (e == kRecSumFlag && has_sum ? 1.0f : 0.0f))));
     }
     if (lane < 2) {
         const uint4 kp = key_piece(s, lane != 0);
@@ -539,7 +547,8 @@ __device__ __forceinline__ float seq_sum_legal(float *row /* LDS, 16-B aligned, 
 // rec_lo / rec_hi: this lane's path node's record (path[lane] / path[64 + lane]) as the select read it
 __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi,
                               uint4 rec_lo, uint4 rec_hi, int k, const uttt_state_t &s, float raw0, float raw1, float v,
-                              int &node_count, bool py = false, float *row = nullptr) {
+                              int &node_count, bool py = false, float *row = nullptr, bool has_sum = false,
+                              float known_sum = 0.0f, float *sum_out = nullptr) {
     const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
@@ -557,12 +566,15 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     float sum = 0.0f;
     if (py) {
         sum = np_sum_f32_legal(p0, p1, b0, b1, L);
+    } else if (has_sum) {
+        sum = known_sum;  // the cache record's (the same values added in the same order at insert)
     } else if (row) {
         sum = seq_sum_legal(row, p0, p1, l0, l1, i0, i1, L);
     } else {
         for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
         for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
     }
+    if (sum_out) *sum_out = sum;
     const float un = 1.0f / (float)L;
     const bool p64 = py && !(sum > 0);  // np.ones(float) / L: float64 priors
     const float q0 = sum > 0 ? p0 / sum : un;
@@ -748,12 +760,18 @@ struct SelClock {
 // independent of every other's, so their latencies overlap instead of running one child after
 // another behind per-child branches. Children past cnt (clamped loads) never win; the compare is the
 // reference's strict '>' in child order.
+// pa >= 0: the previous level's winning action, whose next_state runs while this group's loads are in
+// flight (it was on the critical path between the arg-max and the next level's loads)
 template <int NJ>
 __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int first, int c0, int cnt, float sq, int lane,
-                                           float &best, int &bi, uint4 &bw, SelClock &clk) {
+                                           float &best, int &bi, uint4 &bw, uttt_state_t &s, int &pa, SelClock &clk) {
     uint4 r[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) r[j] = R[first + min(c0 + j * kWave + lane, cnt - 1)];
+    if (pa >= 0) {
+        s = next_state(s, pa);
+        pa = -1;
+    }
     clk.mark<kSpLoad>();
     float v[NJ];
 #pragma unroll
@@ -814,7 +832,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
         const uttt_state_t root = tr.root[t];
         clk.mark<kSpRootState>();
         int sims_done = ctl.sims_done;
-        int budget = kSelectBudget;
+        int budget = tr.budget;
         for (;;) {
             uttt_state_t s = root;
             int node = 0, depth = 0;
@@ -827,6 +845,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             ++trips;
             clk.mark<kSpRoot>();
             bool fail = false;
+            int pa = -1;  // a winning action whose next_state is pending (applied under the next loads)
             for (;;) {
                 const int cnt = PY ? meta_L(nm.x) : link_k(nm.y) * meta_L(nm.x);
                 if (cnt == 0) break;
@@ -846,8 +865,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
                         ++trips;
-                        if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, clk);
-                        else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, clk);
+                        if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
+                        else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                     }
                     bi = __builtin_amdgcn_readlane(wave_argmax_to63(best, bi), 63);
                     if (bi != kNone) {  // the winner's lane holds its record
@@ -918,9 +937,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                         prec_hi = wr;
                     }
                 }
-                s = next_state(s, meta_action(nm.x));
+                if (PY) s = next_state(s, meta_action(nm.x));
+                else pa = meta_action(nm.x);
                 clk.mark<kSpNext>();
             }
+            if (pa >= 0) s = next_state(s, pa);  // the leaf's state
             if (fail) break;
             levels += (unsigned int)(depth + 1);
             const bool lose = is_lose(s);
@@ -960,8 +981,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 trips += 4;
                 // cv doubles as the prior sum's row: its values are in registers before the call
                 const float h0 = cv[lane], h1 = lane < 17 ? cv[64 + lane] : 0.0f, hv = cv[81];
+                const bool hs = !PY && cv[kRecSumFlag] == 1.0f;
                 if (!expand_backup(pool, base, node, depth, path_lo, path_hi, prec_lo, prec_hi, k, s, h0, h1, hv,
-                                   ctl.node_count, PY, cv)) {
+                                   ctl.node_count, PY, cv, hs, cv[kRecSum])) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
                 }
@@ -1199,15 +1221,16 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             }
         }
         const bool cacheable = __ballot(!fin0 || (lane < 17 && !fin1)) == 0ull;
+        float psum = 0.0f;
         if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, pr_lo, pr_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f,
-                           v, ctl.node_count, tr.py != 0, s_row[threadIdx.x >> 6])) {
+                           v, ctl.node_count, tr.py != 0, s_row[threadIdx.x >> 6], false, 0.0f, &psum)) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
             }
             return;
         }
-        inserted = cacheable && cache_insert(cache, s, raw0, raw1, v);
+        inserted = cacheable && cache_insert(cache, s, raw0, raw1, v, tr.py == 0, psum);
         L = (ctl.node_count - nodes_before) / k;
     } else {
         // the reference's exact call pattern: k results, one per queued copy, applied in order
@@ -2096,6 +2119,14 @@ static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, in
     // uttt_mcts.cpp:127: a flush happens once the queue holds batch_size entries,
     // so batch_size <= 1 flushes every queued leaf alone.
     e->tr.batch = batch < 1 ? 1 : batch;
+    // the select budget changes how a move's simulations are spread over launches, never which
+    // simulations run or in what order per tree (results are the same for any value >= 1)
+    static const int budget_env = [] {
+        const char *v = getenv("UTTT_SELECT_BUDGET");
+        const int b = v ? atoi(v) : 0;
+        return b >= 1 && b <= 4096 ? b : kSelectBudget;
+    }();
+    e->tr.budget = budget_env;
     e->phase = 1;
     e->n_pending = 0;
     return UTTT_OK;
