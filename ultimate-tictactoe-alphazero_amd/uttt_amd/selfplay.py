@@ -32,6 +32,7 @@ class HashEvaluator:
     device (Engine.eval_hash_dev), so SelfPlay pipelines its rounds as with the fused network."""
 
     device_count = True
+    cheap = True  # SelfPlay keeps two rounds in flight: the host's reaction, not the kernels, set the pace
 
     def __init__(self, engine):
         self.engine = engine
@@ -117,7 +118,8 @@ class _Lane:
         self.evaluator = None
         self.rounds = 0
         self.finished = 0
-        self.count_host = None  # pinned counts of the round in flight (async rounds, Engine.count_copy)
+        self.count_ring = None  # pinned counts of the rounds in flight (async rounds, Engine.count_copy)
+        self.ring_pos = 0
         self.spec = True        # enqueue the next round's network before its count is known
         self._no_rows = None
 
@@ -286,9 +288,18 @@ class SelfPlay:
                 if progress:
                     progress(self.finished, None)
             return total
+        depth = self._lookahead()
         for ln in self.lanes:
-            if ln.count_host is None:
-                ln.count_host = torch.zeros(3, dtype=torch.int32).pin_memory()
+            if ln.count_ring is None or len(ln.count_ring) < depth + 1:
+                ln.count_ring = [torch.zeros(3, dtype=torch.int32).pin_memory() for _ in range(depth + 1)]
+
+        def fill(ln, q):
+            # rounds in flight per lane: one (the next is enqueued once this one's count is read), or,
+            # with a cheap evaluator, `depth`: the host's reaction then hides under the GPU's work; a
+            # round enqueued past the move's last finds every tree done and changes nothing
+            while len(q) < depth:
+                q.append(self._enqueue_round(ln, ln.spec if depth == 1 else True))
+            return q
 
         state = {}
         for ln in self.lanes:
@@ -298,23 +309,24 @@ class SelfPlay:
                 ln.cur_live = live
                 ln.moves_left = k
                 ln.result_pending = False
-                state[id(ln)] = (ln, self._enqueue_round(ln, ln.spec))
+                state[id(ln)] = (ln, fill(ln, collections.deque()))
         total = moves = 0
         while state:
-            # serve whichever lane's count has landed (polling: waiting on one lane in turn
-            # would leave the other lane's stream empty once it runs ahead)
-            ready = [key for key in state if state[key][1][1].query()]
+            # serve whichever lane's oldest round count has landed (polling: waiting on one lane in
+            # turn would leave the other lane's stream empty once it runs ahead)
+            ready = [key for key in state if state[key][1][0][1].query()]
             if not ready:
                 time.sleep(2e-5)
                 continue
             for key in ready:
-                ln, (rc, ev, spec) = state[key]
+                ln, q = state[key]
+                rc, ev, spec, buf = q.popleft()
                 if ln.result_pending:  # the previous move's end: its counters landed before this count
                     ln.finished, ln.cur_live = ln.engine.move_result()
                     ln.result_pending = False
                     if progress:
                         progress(self.finished, None)
-                n, more = int(ln.count_host[0]), int(ln.count_host[2])
+                n, more = int(buf[0]), int(buf[2])
                 rc.n = n
                 if n > 0:
                     ln.rounds += 1
@@ -330,10 +342,11 @@ class SelfPlay:
                     del state[key]
                     continue
                 if more > 0:  # some tree has simulations left once this round is applied
-                    state[key] = (ln, self._enqueue_round(ln, ln.spec))
+                    fill(ln, q)
                     continue
-                # this round (already enqueued) completes the move: end it and begin the next,
-                # both on the stream, without waiting
+                # this round completes the move (the rounds already enqueued behind it are empty): end
+                # it and begin the next, both on the stream, without waiting
+                q.clear()
                 total += ln.cur_live * self.evaluate_count
                 moves += 1
                 ln.moves_left = None if ln.moves_left is None else ln.moves_left - 1
@@ -347,7 +360,7 @@ class SelfPlay:
                         del state[key]
                         continue
                     ln.engine.move_begin_async()
-                state[key] = (ln, self._enqueue_round(ln, ln.spec))
+                fill(ln, q)
         for ln in self.lanes:  # the last move's counters
             if getattr(ln, "result_pending", False):
                 ln.end_event.synchronize()
@@ -359,22 +372,34 @@ class SelfPlay:
         self.sims += total
         return total
 
+    def _lookahead(self):
+        """Rounds in flight per lane: UTTT_ROUND_LOOKAHEAD, else 2 when every lane's evaluator is cheap
+        (the device hash evaluator: a round's kernels take about as long as the host's reaction to its
+        count, so with one round in flight the GPU idled between rounds), else 1 (a network round is
+        milliseconds: the host keeps up, and an empty look-ahead round would cost its 32 conv launches)."""
+        env = os.environ.get("UTTT_ROUND_LOOKAHEAD")
+        if env:
+            return max(1, int(env))
+        return 2 if all(getattr(ln.evaluator, "cheap", False) for ln in self.lanes) else 1
+
     def _enqueue_round(self, ln, spec):
-        """Select of one round on the lane's stream, its counts copied to ln.count_host right
-        after it, and - speculatively, when the lane's previous round had leaves - the network
-        and apply, all without a host sync. Otherwise (a lane whose rounds are answered by the
-        cache or by terminal positions: the network would run empty) the host enqueues the
-        network once the count shows leaves."""
+        """Select of one round on the lane's stream, its counts copied to a pinned buffer of the lane's
+        ring right after it, and - speculatively, when the lane's previous round had leaves (always,
+        with look-ahead) - the network and apply, all without a host sync. Otherwise (a lane whose
+        rounds are answered by the cache or by terminal positions: the network would run empty) the
+        host enqueues the network once the count shows leaves."""
         rc = RoundCount()
+        buf = ln.count_ring[ln.ring_pos % len(ln.count_ring)]
+        ln.ring_pos += 1
         with self._ctx(ln):
             ln.engine.select_async()
-            ln.engine.count_copy(ln.count_host)
+            ln.engine.count_copy(buf)
             ev = torch.cuda.Event()
             ev.record()
             if spec:
                 p, v = ln.evaluator(None, rc)
                 ln.engine.apply(p, v)
-        return rc, ev, spec
+        return rc, ev, spec, buf
 
     def run(self, game_begin, game_end, seed_base, progress=None):
         self.begin(game_begin, game_end, seed_base)
