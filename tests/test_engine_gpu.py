@@ -154,6 +154,22 @@ def test_selfplay_matches_oracle_and_is_slot_invariant(gpu, oracle_lib):
             assert np.array_equal(r["values"], ref[g]["values"].astype(np.int64))
 
 
+@pytest.mark.parametrize("budget", ["1", "3"])
+def test_select_budget_changes_no_record(gpu, oracle_lib, budget, monkeypatch):
+    """UTTT_SELECT_BUDGET (in-place completions per tree and k_select launch) only spreads a move's
+    simulations over more or fewer launches: records still equal the oracle's bit for bit."""
+    monkeypatch.setenv("UTTT_SELECT_BUDGET", budget)
+    n_games, seed = 8, 606
+    ref = [oracle_lib.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
+    sp = gpu.SelfPlay(8, 30, 4, 1.0, cache_log2=12)
+    sp.run(0, n_games, seed)
+    recs = sp.records()
+    assert len(recs) == n_games
+    for g, r in enumerate(recs):
+        assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (budget, g)
+        assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64)), (budget, g)
+
+
 @pytest.mark.parametrize("tau", [0.0, 0.5, 2.0])
 def test_selfplay_other_temperatures_match_oracle(gpu, oracle_lib, tau):
     """k_move_end's one-hot (tau 0) and pow (tau != 1) score paths against the oracle's

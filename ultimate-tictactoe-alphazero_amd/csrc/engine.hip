@@ -1436,7 +1436,7 @@ struct Slot {
     int64_t fin_game;
     int64_t fin_offset;  // arena row of its first ply
     int32_t fin_value;   // value of ply 0 (self_play_cpp.py:95)
-    int32_t pad;
+    int32_t seed_pending;  // 1: k_finalize gave the slot a new game whose MT19937 key k_archive seeds
 };
 
 struct GameEntry {
@@ -1768,7 +1768,10 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
                 sl.game = g;
                 sl.ply = 0;
                 sl.live = 1;
-                mt_seed(sp.mt_key + (size_t)i * 624, sp.mt_pos + i, sp.seed_base + (uint32_t)g);
+                // the key is seeded by k_archive (one block per slot, so the ~1 in 40 slots refilled per
+                // move seed on their own CUs): 624 dependent steps and 624 strided stores per new game
+                // on this kernel's single CU were most of its time (round 4)
+                sl.seed_pending = 1;
             } else {
                 sl.game = -1;
             }
@@ -1788,11 +1791,16 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
 }
 
 // Copy each just-finished game's plies to its arena rows, with values
-// (self_play_cpp.py:95-99: ply 0 gets the final value, then alternating).
+// (self_play_cpp.py:95-99: ply 0 gets the final value, then alternating), and seed the MT19937
+// key of a slot k_finalize gave a new game (numpy's init_genrand(seed_base + game)).
 __global__ void k_archive(SelfPlay sp, const unsigned long long *err) {
     if (err && *err != ~0ull) return;
     const int s = blockIdx.x;
     const Slot &sl = sp.slot[s];
+    if (sl.seed_pending && threadIdx.x == 0) {
+        mt_seed(sp.mt_key + (size_t)s * 624, sp.mt_pos + s, sp.seed_base + (uint32_t)sl.game);
+        sp.slot[s].seed_pending = 0;
+    }
     if (!sl.finished || sl.fin_offset < 0) return;
     for (int i = threadIdx.x; i < sl.fin_len * 81; i += blockDim.x) {
         const int ply = i / 81, a = i % 81;
@@ -2121,12 +2129,9 @@ static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, in
     e->tr.batch = batch < 1 ? 1 : batch;
     // the select budget changes how a move's simulations are spread over launches, never which
     // simulations run or in what order per tree (results are the same for any value >= 1)
-    static const int budget_env = [] {
-        const char *v = getenv("UTTT_SELECT_BUDGET");
-        const int b = v ? atoi(v) : 0;
-        return b >= 1 && b <= 4096 ? b : kSelectBudget;
-    }();
-    e->tr.budget = budget_env;
+    const char *bv = getenv("UTTT_SELECT_BUDGET");
+    const int b = bv ? atoi(bv) : 0;
+    e->tr.budget = b >= 1 && b <= 4096 ? b : kSelectBudget;
     e->phase = 1;
     e->n_pending = 0;
     return UTTT_OK;
@@ -2438,6 +2443,7 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     int64_t ctr[4] = {game_begin, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const unsigned long long *)nullptr);
+    hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, sp, (const unsigned long long *)nullptr);
     if ((rc = check_launch())) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_move, sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
