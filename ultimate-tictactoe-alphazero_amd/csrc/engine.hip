@@ -237,7 +237,8 @@ UTTT_DPP_STEP(v_min_u32, hm)
 UTTT_DPP_STEP(v_min_u32, rm)
 UTTT_DPP_STEP(v_min_u32, b15)
 UTTT_DPP_STEP(v_min_u32, b31)
-__device__ __forceinline__ int wave_argmax_to63(float v, int i) {
+// wave-uniform result: the index of the largest v, the lowest index among equal maxima
+__device__ __forceinline__ int wave_argmax_u(float v, int i) {
     // the value as an order-preserving unsigned (-0 canonicalised to +0 first), so each step of the max
     // is an integer max (no float canonicalisation)
     uint32_t b = __float_as_uint(v + 0.0f);
@@ -251,6 +252,9 @@ __device__ __forceinline__ int wave_argmax_to63(float v, int i) {
     v_max_u32_b31(m);  // row_bcast31 -> rows 2, 3
     asm volatile("s_nop 1");  // the asm's VALU write before the compiler's reads of m
     const uint32_t top = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+    // the usual case: one lane holds the maximum, and its index is the answer (no second pass)
+    const uint64_t at = __ballot(b == top);
+    if (__popcll(at) == 1) return __builtin_amdgcn_readlane(i, __builtin_ctzll(at));
     uint32_t k = b == top ? (uint32_t)i : (uint32_t)kNone;  // indices are >= 0: unsigned min is the int min
     v_min_u32_q1(k);
     v_min_u32_q2(k);
@@ -259,7 +263,7 @@ __device__ __forceinline__ int wave_argmax_to63(float v, int i) {
     v_min_u32_b15(k);
     v_min_u32_b31(k);
     asm volatile("s_nop 1");
-    return (int)k;
+    return __builtin_amdgcn_readlane((int)k, 63);
 }
 
 // Orders this wave's global stores before its later global loads (other lanes
@@ -868,7 +872,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                         if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                         else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                     }
-                    bi = __builtin_amdgcn_readlane(wave_argmax_to63(best, bi), 63);
+                    bi = wave_argmax_u(best, bi);
                     if (bi != kNone) {  // the winner's lane holds its record
                         const int wl = bi & (kWave - 1);
                         wr = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)bw.x, wl),

@@ -344,8 +344,11 @@ class SelfPlay:
                 if more > 0:  # some tree has simulations left once this round is applied
                     fill(ln, q)
                     continue
-                # this round completes the move (the rounds already enqueued behind it are empty): end
-                # it and begin the next, both on the stream, without waiting
+                # this round completes the move (the rounds already enqueued behind it are empty: no
+                # tree has a simulation left, so their counts are 0): end it and begin the next, both on
+                # the stream, without waiting
+                for rc_empty, *_ in q:
+                    rc_empty.n = 0
                 q.clear()
                 total += ln.cur_live * self.evaluate_count
                 moves += 1
