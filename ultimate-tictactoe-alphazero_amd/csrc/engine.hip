@@ -672,7 +672,7 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const utt
 // (pending = 2) and resumes in the next launch from the same point: the sequence of
 // simulations per tree, hence every result, is unchanged; only the tail of the launch is cut.
 constexpr int kSelectBudget = 8;
-constexpr int kScanGroup = 4;  // child-scan iterations (64 children each) whose loads are issued together
+constexpr int kScanGroup = 8;  // child-scan iterations (64 children each) whose loads are issued together (at most)
 
 // k_select phase clock. Product build: empty (every call compiles to nothing). Diagnostics engine
 // build (-DUTTT_DIAG_BUILD, libuttt_engine_diag.so, tools/diag/select_cycles.py): each mark drains the
@@ -869,7 +869,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
                         ++trips;
+                        // the smallest group that covers what is left (a node of a k = 8 flush has up to 648
+                        // children: one round trip instead of three)
                         if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
+                        else if (cnt - c0 <= 4 * kWave) puct_group<4>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                         else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                     }
                     bi = wave_argmax_u(best, bi);
