@@ -149,6 +149,12 @@ int uttt_search_select_async(uttt_engine_t *eng);
 int uttt_search_count_copy(uttt_engine_t *eng, int32_t *dst);
 /* Device address of the round's counts. */
 int uttt_search_count_ptr(uttt_engine_t *eng, const int32_t **count);
+/* uttt_search_select_async whose scan also stores the three counts into slot ring_slot (0..7) of
+ * the engine's host-visible count ring (fine-grained pinned memory, system-scope stores): the host
+ * reads them once an event recorded after this call has completed, with no copy on the stream. */
+int uttt_search_select_async_to(uttt_engine_t *eng, int32_t ring_slot);
+/* The count ring: *ring = n_slots x {pending, stopped, left after apply, unused} int32, host memory. */
+int uttt_search_count_ring(uttt_engine_t *eng, const int32_t **ring, int32_t *n_slots);
 
 /* Host copies of the pending leaves (slot order) and their multiplicity k
  * (the number of identical copies the reference would have queued). */

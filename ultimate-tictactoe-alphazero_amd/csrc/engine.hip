@@ -121,6 +121,7 @@ struct Pool {
     int64_t cap;
 };
 constexpr int kMaxSimsRec = 4095;
+constexpr int kCountRing = 8;  // host-visible count slots per engine (uttt_search_select_async_to)
 
 struct Trees {
     TreeCtl *ctl;
@@ -617,13 +618,18 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
 
 // ----------------------------------------------------------- root (begin) --
 // uttt_mcts.cpp:92-103: root expanded at once with uniform priors 1.0f/|legal|.
-// Self-play passes `live` (slot flags); search passes nullptr (all live).
-__global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const uttt_state_t *src, const int32_t *live) {
+// Self-play passes `live` (slot flags) and the slots' states in place (src_stride = sizeof(Slot)),
+// and err: the asynchronous move end's failure word, reset here (once per move, before this move's
+// k_tree_err, after the previous move end's read of it) instead of by a memset on the stream;
+// search passes nullptr (all live) and packed states.
+__global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const char *src, int src_stride, const int32_t *live,
+                                                  unsigned long long *err) {
     const int lane = lane_id();
     const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (err && t == 0 && lane == 0) *err = ~0ull;
     if (t >= tr.n_trees) return;
     const bool on = live ? (live[t] != 0) : true;
-    const uttt_state_t s = src[t];
+    const uttt_state_t s = *reinterpret_cast<const uttt_state_t *>(src + (size_t)t * src_stride);
     const size_t base = (size_t)t * pool.cap;
     uint32_t m[3];
     legal_mask(s, m);
@@ -1084,7 +1090,10 @@ __device__ __forceinline__ T block_scan_1024(T v, T *total, T *wsum /* __shared_
 }
 
 // One block: exclusive scan of pending flags -> tree_of[slot] in tree order.
-__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats) {
+// host_count (optional): the three counts are also stored to this host-visible (fine-grained pinned)
+// word triple at system scope, so the host reads a round's counts when the round's event completes
+// without a copy operation on the stream (round 4: one stream operation less per round)
+__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count) {
     __shared__ unsigned long long wsum[16];
     const int tid = threadIdx.x;
     if (stats && tid < 64) {  // the select launch before this scan is complete: fold its slowest tree
@@ -1130,9 +1139,16 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
         }
     }
     if (tid == 0) {
-        tr.count[0] = (int)(tot & 0x1FFFFFull);
-        tr.count[1] = (int)((tot >> 21) & 0x1FFFFFull);
-        tr.count[2] = (int)(tot >> 42);  // trees with simulations left after this round (0: the search ends with it)
+        const int c0 = (int)(tot & 0x1FFFFFull), c1 = (int)((tot >> 21) & 0x1FFFFFull);
+        const int c2 = (int)(tot >> 42);  // trees with simulations left after this round (0: the search ends with it)
+        tr.count[0] = c0;
+        tr.count[1] = c1;
+        tr.count[2] = c2;
+        if (host_count) {
+            __hip_atomic_store(host_count + 0, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_count + 1, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_count + 2, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1721,9 +1737,17 @@ __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, con
 
 // One block: give finished games arena rows (slot order) and free slots the
 // next game ids (slot order) — deterministic for a given slot count.
-__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned long long *err) {
+// host_move (optional, fine-grained pinned): the counters after this move end and the failure word,
+// stored at system scope by the kernel itself (the asynchronous move end: no copies on the stream)
+__device__ __forceinline__ void store_host_i64(int64_t *p, int64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned long long *err, int64_t *host_move) {
     __shared__ unsigned long long wsum[16];
-    if (err && *err != ~0ull) return;  // a failed tree: the move is not ended (k_move_end)
+    if (err && *err != ~0ull) {  // a failed tree: the move is not ended (k_move_end)
+        if (host_move && threadIdx.x == 0) store_host_i64(host_move + 4, (int64_t)*err);
+        return;
+    }
     const int tid = threadIdx.x;
     const int per = (sp.slots + 1023) / 1024;
     const int b = tid * per, e = min(b + per, sp.slots);
@@ -1794,6 +1818,10 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
         sp.ctr[0] = nxt < sp.game_end ? nxt : sp.game_end;
         // live slots for the next move: those still playing plus the free ones given a game
         sp.ctr[3] = (int64_t)(sp.slots - free_total) + (sp.ctr[0] - next0);
+        if (host_move) {
+            for (int i = 0; i < 4; ++i) store_host_i64(host_move + i, sp.ctr[i]);
+            store_host_i64(host_move + 4, (int64_t)~0ull);
+        }
     }
 }
 
@@ -1851,6 +1879,7 @@ struct uttt_engine {
     Pool pool{};
     Trees tr{};
     int32_t *h_count = nullptr;  // pinned
+    int32_t *h_ring = nullptr;   // fine-grained pinned: kCountRing x {pending, stopped, left, pad}, k_scan-written
     int32_t *d_rowbase = nullptr;
     float *d_pol_scratch = nullptr;
     float *d_val_scratch = nullptr;
@@ -2062,10 +2091,15 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->d_cache_ctr, 4 * kRow)))
         return fail(rc);
     if ((rc = alloc_n(e, &e->d_err, 1))) return fail(rc);
-    if (hipHostMalloc((void **)&e->h_move, sizeof(int64_t) * 5, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void **)&e->h_move, sizeof(int64_t) * 5, hipHostMallocCoherent) != hipSuccess) {
         set_error("hipHostMalloc failed");
         return fail(UTTT_ERR_HIP);
     }
+    if (hipHostMalloc((void **)&e->h_ring, sizeof(int32_t) * 4 * kCountRing, hipHostMallocCoherent) != hipSuccess) {
+        set_error("hipHostMalloc failed");
+        return fail(UTTT_ERR_HIP);
+    }
+    memset(e->h_ring, 0, sizeof(int32_t) * 4 * kCountRing);
     if (hipHostMalloc((void **)&e->h_count, sizeof(int32_t) * 4, hipHostMallocDefault) != hipSuccess) {
         set_error("hipHostMalloc failed");
         return fail(UTTT_ERR_HIP);
@@ -2097,6 +2131,7 @@ int uttt_engine_destroy(uttt_engine_t *e) {
         if (e->cache.rec) (void)hipFree(e->cache.rec);
     }
     if (e->h_count) (void)hipHostFree(e->h_count);
+    if (e->h_ring) (void)hipHostFree(e->h_ring);
     if (e->h_move) (void)hipHostFree(e->h_move);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -2161,7 +2196,8 @@ int uttt_search_begin_mode(uttt_engine_t *e, const uttt_state_t *roots, int32_t 
     e->selfplay = false;
     HIP_TRY(hipMemcpyAsync(e->tr.leaf, roots, sizeof(uttt_state_t) * n_trees, hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_begin, dim3(grid_waves(n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
-                       (const uttt_state_t *)e->tr.leaf, (const int32_t *)nullptr);
+                       (const char *)e->tr.leaf, (int)sizeof(uttt_state_t), (const int32_t *)nullptr,
+                       (unsigned long long *)nullptr);
     return check_launch();
 }
 
@@ -2185,7 +2221,8 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
         if ((rc = check_launch())) return rc;
         {
             TimedLaunch tl(e, kKScan);
-            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr);
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr,
+                               (int32_t *)nullptr);
         }
         if ((rc = check_launch())) return rc;
         HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
@@ -2206,7 +2243,25 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     return UTTT_OK;
 }
 
-int uttt_search_select_async(uttt_engine_t *e) {
+static int select_async_impl(uttt_engine_t *e, int32_t *host_count);
+int uttt_search_select_async(uttt_engine_t *e) { return select_async_impl(e, nullptr); }
+
+int uttt_search_select_async_to(uttt_engine_t *e, int32_t ring_slot) {
+    if (!e || ring_slot < 0 || ring_slot >= kCountRing) {
+        set_error("uttt_search_select_async_to: ring slot must be in 0..%d", kCountRing - 1);
+        return UTTT_ERR_ARG;
+    }
+    return select_async_impl(e, e->h_ring + 4 * ring_slot);
+}
+
+int uttt_search_count_ring(uttt_engine_t *e, const int32_t **ring, int32_t *n_slots) {
+    if (!e || !ring || !n_slots) return UTTT_ERR_ARG;
+    *ring = e->h_ring;
+    *n_slots = kCountRing;
+    return UTTT_OK;
+}
+
+static int select_async_impl(uttt_engine_t *e, int32_t *host_count) {
     if (!e) return UTTT_ERR_ARG;
     if (e->phase != 1) {
         set_error("uttt_search_select_async: call uttt_search_begin (or apply the previous round) first");
@@ -2222,7 +2277,8 @@ int uttt_search_select_async(uttt_engine_t *e) {
     if ((rc = check_launch())) return rc;
     {
         TimedLaunch tl(e, kKScan);
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr,
+                           host_count);
     }
     if ((rc = check_launch())) return rc;
     e->n_pending = -1;
@@ -2449,7 +2505,8 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipMemsetAsync(sp.slot, 0, sizeof(Slot) * slots, e->stream));
     int64_t ctr[4] = {game_begin, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const unsigned long long *)nullptr);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const unsigned long long *)nullptr,
+                       (int64_t *)nullptr);
     hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, sp, (const unsigned long long *)nullptr);
     if ((rc = check_launch())) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_move, sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
@@ -2481,11 +2538,9 @@ int uttt_selfplay_move_begin(uttt_engine_t *e, int32_t *n_live) {
     int nl = 0;
     for (int v : live) nl += v != 0;
     if (n_live) *n_live = nl;
-    // gather roots: states are strided inside Slot; copy via a tiny 2D memcpy
-    HIP_TRY(hipMemcpy2DAsync(e->tr.leaf, sizeof(uttt_state_t), e->sp.slot, sizeof(Slot), sizeof(uttt_state_t), slots,
-                             hipMemcpyDeviceToDevice, e->stream));
+    // roots: the slots' states, read in place (Slot.state is the first member)
     hipLaunchKernelGGL(k_begin, dim3(grid_waves(slots)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
-                       (const uttt_state_t *)e->tr.leaf, (const int32_t *)e->sp.live);
+                       (const char *)e->sp.slot, (int)sizeof(Slot), (const int32_t *)e->sp.live, e->d_err);
     int rc = check_launch();
     if (rc) return rc;
     e->phase = 1;
@@ -2510,7 +2565,7 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
         TimedLaunch tl(e, kKMoveEnd);
         const unsigned long long *no_err = nullptr;
         hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, no_err);
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, no_err);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, no_err, (int64_t *)nullptr);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, no_err);
     }
     if ((rc = check_launch())) return rc;
@@ -2545,10 +2600,8 @@ int uttt_selfplay_move_begin_async(uttt_engine_t *e) {
     const int slots = e->sp.slots;
     e->tr.n_trees = slots;
     e->moves++;
-    HIP_TRY(hipMemcpy2DAsync(e->tr.leaf, sizeof(uttt_state_t), e->sp.slot, sizeof(Slot), sizeof(uttt_state_t), slots,
-                             hipMemcpyDeviceToDevice, e->stream));
     hipLaunchKernelGGL(k_begin, dim3(grid_waves(slots)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
-                       (const uttt_state_t *)e->tr.leaf, (const int32_t *)e->sp.live);
+                       (const char *)e->sp.slot, (int)sizeof(Slot), (const int32_t *)e->sp.live, e->d_err);
     int rc = check_launch();
     if (rc) return rc;
     e->phase = 1;
@@ -2567,8 +2620,7 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
     }
     HIP_TRY(hipSetDevice(e->device));
     const int slots = e->sp.slots;
-    HIP_TRY(hipMemsetAsync(e->d_err, 0xFF, sizeof(unsigned long long), e->stream));
-    {
+    {  // d_err was reset by this move's k_begin
         TimedLaunch tl(e, kKMoveEnd);
         // a failed tree leaves the whole move unended (k_tree_err -> *d_err; the kernels behind it
         // check it), so the engine is in the state the blocking move end refuses in
@@ -2576,13 +2628,11 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
                            slots, e->d_err);
         const unsigned long long *err = e->d_err;
         hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, err);
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, err);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, err, e->h_move);
         hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, err);
     }
     int rc = check_launch();
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(e->h_move, e->sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->h_move + 4, e->d_err, sizeof(int64_t), hipMemcpyDeviceToHost, e->stream));
+    if (rc) return rc;  // k_finalize stored the counters and the failure word into h_move
     e->phase = 0;
     return UTTT_OK;
 }

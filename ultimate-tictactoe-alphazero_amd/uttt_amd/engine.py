@@ -120,6 +120,19 @@ class Engine:
         check(self.lib.uttt_search_select_async(self.h))
         self.n_pending = None
 
+    def select_async_to(self, ring_slot):
+        """select_async whose scan also writes the round's counts into slot ring_slot of the engine's
+        host-visible ring (count_ring()): readable once an event recorded after it has completed."""
+        check(self.lib.uttt_search_select_async_to(self.h, int(ring_slot)))
+        self.n_pending = None
+
+    def count_ring(self):
+        """The engine's host count ring as an (n_slots, 4) int32 numpy view of pinned host memory."""
+        p, n = ctypes.c_void_p(), ctypes.c_int32()
+        check(self.lib.uttt_search_count_ring(self.h, ctypes.byref(p), ctypes.byref(n)))
+        arr = ctypes.cast(p, ctypes.POINTER(ctypes.c_int32 * (4 * n.value))).contents
+        return np.frombuffer(arr, dtype=np.int32).reshape(n.value, 4)
+
     def count_copy(self, dst):
         """Enqueue a copy of the round's [pending, stopped, trees with simulations left after
         this round] counts into dst (pinned int32 host tensor of >= 3)."""

@@ -290,8 +290,10 @@ class SelfPlay:
             return total
         depth = self._lookahead()
         for ln in self.lanes:
-            if ln.count_ring is None or len(ln.count_ring) < depth + 1:
-                ln.count_ring = [torch.zeros(3, dtype=torch.int32).pin_memory() for _ in range(depth + 1)]
+            if ln.count_ring is None:
+                ln.count_ring = ln.engine.count_ring()  # the scan writes each round's counts here
+            if len(ln.count_ring) < depth + 1:
+                raise ValueError(f"round look-ahead {depth} needs {depth + 1} count slots")
 
         def fill(ln, q):
             # rounds in flight per lane: one (the next is enqueued once this one's count is read), or,
@@ -386,17 +388,17 @@ class SelfPlay:
         return 2 if all(getattr(ln.evaluator, "cheap", False) for ln in self.lanes) else 1
 
     def _enqueue_round(self, ln, spec):
-        """Select of one round on the lane's stream, its counts copied to a pinned buffer of the lane's
-        ring right after it, and - speculatively, when the lane's previous round had leaves (always,
+        """Select of one round on the lane's stream, its counts stored by the scan into a slot of the
+        engine's host count ring (no copy operation), and - speculatively, when the lane's previous round had leaves (always,
         with look-ahead) - the network and apply, all without a host sync. Otherwise (a lane whose
         rounds are answered by the cache or by terminal positions: the network would run empty) the
         host enqueues the network once the count shows leaves."""
         rc = RoundCount()
-        buf = ln.count_ring[ln.ring_pos % len(ln.count_ring)]
+        slot = ln.ring_pos % len(ln.count_ring)
+        buf = ln.count_ring[slot]
         ln.ring_pos += 1
         with self._ctx(ln):
-            ln.engine.select_async()
-            ln.engine.count_copy(buf)
+            ln.engine.select_async_to(slot)
             ev = torch.cuda.Event()
             ev.record()
             if spec:
