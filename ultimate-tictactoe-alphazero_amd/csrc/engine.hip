@@ -553,7 +553,7 @@ __device__ __forceinline__ float seq_sum_legal(float *row /* LDS, 16-B aligned, 
 __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth, int path_lo, int path_hi,
                               uint4 rec_lo, uint4 rec_hi, int k, const uttt_state_t &s, float raw0, float raw1, float v,
                               int &node_count, bool py = false, float *row = nullptr, bool has_sum = false,
-                              float known_sum = 0.0f, float *sum_out = nullptr) {
+                              float known_sum = 0.0f, float *sum_out = nullptr, uint4 *root_out = nullptr) {
     const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
@@ -596,8 +596,7 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
     // children carry float64 priors when the policy summed to zero (kMetaP64)
     const uint32_t leaf_meta = (uint32_t)L << 23 | (py ? (kMetaWF32 | (p64 ? kMetaP64 : 0u)) : 0u);
     const uint32_t leaf_link = make_link((uint32_t)nb, (uint32_t)k);
-    auto update = [&](uint4 r, int pn, int d) {  // path node pn at depth d, its record r
-
+    auto update = [&](uint4 r, int pn, int d) -> uint4 {  // path node pn at depth d, its record r
         float w = __uint_as_float(r.x);
         const float x = ((depth - d) & 1) ? -v : v;
         for (int j = 0; j < k; ++j) w += x;
@@ -609,9 +608,16 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
             r.w = leaf_link;
         }
         pool.rec[base + pn] = r;
+        return r;
     };
-    if (lane <= depth) update(rec_lo, path_lo, lane);
+    uint4 new_lo = rec_lo;
+    if (lane <= depth) new_lo = update(rec_lo, path_lo, lane);
     if (lane + 64 <= depth) update(rec_hi, path_hi, lane + 64);
+    if (root_out)  // the root's record as just written (lane 0 holds path[0])
+        *root_out = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)new_lo.x, 0),
+                               (uint32_t)__builtin_amdgcn_readlane((int)new_lo.y, 0),
+                               (uint32_t)__builtin_amdgcn_readlane((int)new_lo.z, 0),
+                               (uint32_t)__builtin_amdgcn_readlane((int)new_lo.w, 0));
     node_count = nb + blocks * L;
     return true;
 }
@@ -678,7 +684,7 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const cha
 // (pending = 2) and resumes in the next launch from the same point: the sequence of
 // simulations per tree, hence every result, is unchanged; only the tail of the launch is cut.
 constexpr int kSelectBudget = 8;
-constexpr int kScanGroup = 8;  // child-scan iterations (64 children each) whose loads are issued together (at most)
+constexpr int kScanGroup = 4;  // child-scan iterations (64 children each) whose loads are issued together
 
 // k_select phase clock. Product build: empty (every call compiles to nothing). Diagnostics engine
 // build (-DUTTT_DIAG_BUILD, libuttt_engine_diag.so, tools/diag/select_cycles.py): each mark drains the
@@ -843,16 +849,20 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
         clk.mark<kSpRootState>();
         int sims_done = ctl.sims_done;
         int budget = tr.budget;
+        // the root's record after this wave's own last back-up (no other wave writes this tree's
+        // nodes during the launch): later descents start from it instead of reloading R[0]
+        uint4 root_rec = make_uint4(0u, 0u, 0u, 0u);
+        bool root_known = false;
         for (;;) {
             uttt_state_t s = root;
             int node = 0, depth = 0;
             int path_lo = 0, path_hi = 0;  // lane d: path[d], path[64 + d]
             // the current node's meta (visits, action, L) and link (below the root: from the parent's scan)
-            const uint4 r0 = R[0];
+            const uint4 r0 = root_known ? root_rec : R[0];
             uint2 nm = make_uint2(r0.z, r0.w);
             // lane d: the record of path[d] (prec_lo) and path[64 + d] (prec_hi) as read on the way down
             uint4 prec_lo = r0, prec_hi = make_uint4(0u, 0u, 0u, 0u);
-            ++trips;
+            trips += root_known ? 0u : 1u;
             clk.mark<kSpRoot>();
             bool fail = false;
             int pa = -1;  // a winning action whose next_state is pending (applied under the next loads)
@@ -875,10 +885,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                     // memory after the arg-max: one dependent round trip per level.
                     for (int c0 = 0; c0 < cnt; c0 += kScanGroup * kWave) {
                         ++trips;
-                        // the smallest group that covers what is left (a node of a k = 8 flush has up to 648
-                        // children: one round trip instead of three)
                         if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
-                        else if (cnt - c0 <= 4 * kWave) puct_group<4>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                         else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                     }
                     bi = wave_argmax_u(best, bi);
@@ -964,13 +971,20 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 // Terminal: search_leaf returns -(is_lose ? -1 : 0) (uttt_mcts.cpp:19-22),
                 // backpropagate adds it at the leaf and flips sign upwards (:47-54).
                 const float v = -(lose ? -1.0f : 0.0f);
-                auto backup1 = [&](uint4 r, int pn, int d) {  // from the record read on the way down
+                auto backup1 = [&](uint4 r, int pn, int d) -> uint4 {  // from the record read on the way down
                     r.x = __float_as_uint(__uint_as_float(r.x) + (((depth - d) & 1) ? -v : v));
                     r.z += 1u;
                     R[pn] = r;
+                    return r;
                 };
-                if (lane <= depth) backup1(prec_lo, path_lo, lane);
+                uint4 nl = prec_lo;
+                if (lane <= depth) nl = backup1(prec_lo, path_lo, lane);
                 if (lane + 64 <= depth) backup1(prec_hi, path_hi, lane + 64);
+                root_rec = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)nl.x, 0),
+                                      (uint32_t)__builtin_amdgcn_readlane((int)nl.y, 0),
+                                      (uint32_t)__builtin_amdgcn_readlane((int)nl.z, 0),
+                                      (uint32_t)__builtin_amdgcn_readlane((int)nl.w, 0));
+                root_known = true;
                 wave_memory_fence();
                 trips += 2;
                 bytes += 16ull * (unsigned long long)(depth + 1);
@@ -996,10 +1010,11 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                 const float h0 = cv[lane], h1 = lane < 17 ? cv[64 + lane] : 0.0f, hv = cv[81];
                 const bool hs = !PY && cv[kRecSumFlag] == 1.0f;
                 if (!expand_backup(pool, base, node, depth, path_lo, path_hi, prec_lo, prec_hi, k, s, h0, h1, hv,
-                                   ctl.node_count, PY, cv, hs, cv[kRecSum])) {
+                                   ctl.node_count, PY, cv, hs, cv[kRecSum], nullptr, &root_rec)) {
                     if (lane == 0) ctl.status |= kErrCapacity;
                     break;
                 }
+                root_known = true;
                 clk.mark<kSpExpand>();
                 wave_memory_fence();
                 ++hits;
