@@ -40,6 +40,7 @@ for s in $STEPS; do
     tprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tprof -o train \
                -- python3 tools/bench_train.py --variants ${TPROF_VARIANT:-graph_f16} --epochs 1 --samples 8192 --cpu-steps 0 \
                > $OUT/tprof.log 2>&1 ;;
+    dups)  timeout -k 10 300 python -u tools/diag/round_duplicates.py ${DUPS_ARGS:-} > $OUT/round_duplicates.log 2>&1 ;;
     selcyc) timeout -k 10 300 python -u tools/diag/select_cycles.py ${SELCYC_ARGS:-} > $OUT/select_cycles.log 2>&1 ;;
     pretouch) for m in 0 1 2 3; do  # k_select's first root load: TLB or line? (engine.hip g_sel_pretouch)
                 timeout -k 10 300 python -u tools/diag/select_cycles.py 100 10 $m > $OUT/pretouch_$m.log 2>&1 || exit $?
