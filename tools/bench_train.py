@@ -53,7 +53,11 @@ def main():
               "graph_f16_cl": dict(graph=True, precision="f16", channels_last=True),
               # the per-rank shard of the global batch 128 on 8 data-parallel ranks (DESIGN §7c projection)
               "graph_b16": dict(graph=True, batch_size=16),
-              "graph_tuned": dict(graph=True, tune=True), "graph_cl_tuned": dict(graph=True, channels_last=True, tune=True)}[var]
+              "graph_tuned": dict(graph=True, tune=True), "graph_cl_tuned": dict(graph=True, channels_last=True, tune=True),
+              # the graph step's optimizer: fused Adam (the default from round 4) against foreach
+              "graph_foreach": dict(graph=True, tune=True, adam="foreach"),
+              "graph_fused": dict(graph=True, tune=True, adam="fused"),
+              "graph_b16_fused": dict(graph=True, batch_size=16, adam="fused")}[var]
         model = random_network(0)
         train.train_network(model, h[:1024], epochs=1, device=dev, log=None, **kw)  # warm-up (MIOpen tuning)
         model = random_network(0)

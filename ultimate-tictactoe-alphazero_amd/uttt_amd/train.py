@@ -200,7 +200,7 @@ def _use_graph(graph, device, world):
 
 
 def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, device=None, seed=0, lr=0.001,
-                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=None):
+                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=None, adam=None):
     """Train `model` (a DualNetwork) on `history` in place; returns the per-epoch mean losses.
     In a torch.distributed job every rank calls this with the same history and seed.
     graph (default on for one GPU; UTTT_TRAIN_GRAPH=0 disables): replay the step as a HIP graph
@@ -215,8 +215,12 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
     if tune is None:  # MIOpen find before the capture (round 4: graph fp32 13.0k -> 16.3k samples/s)
         import os
         tune = os.environ.get("UTTT_TRAIN_TUNE", "1") != "0"
+    if adam is None:  # the graph step's Adam: "fused" (default) or "foreach" (rounds 1-3 for fp32)
+        import os
+        adam = os.environ.get("UTTT_TRAIN_ADAM", "fused")
     if _use_graph(graph, device, world):
-        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision, tune)
+        return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision, tune,
+                              adam)
     if precision != "fp32":
         raise ValueError("precision other than fp32 needs the graph step (one GPU)")
     net = prepare(model, device, sync_bn)
@@ -243,13 +247,19 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
 
 
 def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision="fp32",
-                   tune=False):
+                   tune=False, adam="fused"):
     net = model.to(device)
     if channels_last:
         net = net.to(memory_format=torch.channels_last)
     net.train()
     lr_t = torch.tensor(lr, dtype=torch.float32, device=device)
-    if precision == "f16":  # the fused kernel takes found_inf (skips the step on the device)
+    # the fused Adam kernel for both precisions (f16: it also takes found_inf and skips the step on the
+    # device). Round 4: the fp32 step used foreach=True, which with capturable=True and a tensor lr ran
+    # ~800 per-parameter kernels per step (222 of them divisions, ~1 ms of the 7.9 ms step in the trace,
+    # profiles/r4/train_fp32_graph_tuned_kernel_stats.csv); the update is the same algorithm
+    if adam not in ("fused", "foreach"):
+        raise ValueError("adam must be 'fused' or 'foreach'")
+    if adam == "fused" or precision == "f16":
         opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, fused=True)
     else:
         opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, foreach=True)
