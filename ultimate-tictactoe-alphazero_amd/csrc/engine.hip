@@ -191,18 +191,6 @@ __device__ __forceinline__ void wave_argmax_d(double &v, int &i) {
     }
 }
 
-__device__ __forceinline__ void wave_argmax(float &v, int &i) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float ov = __shfl_xor(v, off);
-        const int oi = __shfl_xor(i, off);
-        if (ov > v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
-    }
-}
-
 __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -239,7 +227,7 @@ UTTT_DPP_STEP(v_min_u32, rm)
 UTTT_DPP_STEP(v_min_u32, b15)
 UTTT_DPP_STEP(v_min_u32, b31)
 // wave-uniform result: the index of the largest v, the lowest index among equal maxima
-__device__ __forceinline__ int wave_argmax_u(float v, int i) {
+__device__ __forceinline__ int wave_argmax(float v, int i) {
     // the value as an order-preserving unsigned (-0 canonicalised to +0 first), so each step of the max
     // is an integer max (no float canonicalisation)
     uint32_t b = __float_as_uint(v + 0.0f);
@@ -888,7 +876,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
                         if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                         else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                     }
-                    bi = wave_argmax_u(best, bi);
+                    bi = wave_argmax(best, bi);
                     if (bi != kNone) {  // the winner's lane holds its record
                         const int wl = bi & (kWave - 1);
                         wr = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)bw.x, wl),
