@@ -350,27 +350,12 @@ __device__ __forceinline__ rsrc_t rec_rsrc(const EvalCache &c, uint32_t slot) {
 // record read in one round trip (lanes 0-1 the key, checked against s; 2-22 the values), then the
 // flag is re-checked. On a hit the 82 values are copied to dst (LDS, 16-byte aligned, >= 84 floats)
 // and true is returned; a tag that matched another position's entry (a 16-bit collision) is a miss.
-// The probe's first round trip, issued on its own (k_select issues it before its leaf checks, whose
-// latency then hides under the load): h64 the position's hash, f the kProbe flags (lanes 0..kProbe-1).
-struct CacheProbe {
-    uint64_t h64;
-    uint32_t f;
-};
-__device__ __forceinline__ CacheProbe cache_probe_issue(const EvalCache &c, const uttt_state_t &s) {
-    CacheProbe p{0ull, 0u};
-    if (!c.flag) return p;
-    const int lane = (int)(threadIdx.x & 63);
-    p.h64 = state_hash64(s);
-    const uint32_t h = (uint32_t)p.h64;
-    p.f = lane < kProbe ? ld_agent(c.flag + ((h + (uint32_t)lane) & c.mask)) : 0u;
-    return p;
-}
-__device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *dst, const CacheProbe &pr) {
+__device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *dst) {
     if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
-    const uint64_t h64 = pr.h64;
+    const uint64_t h64 = state_hash64(s);
     const uint32_t h = (uint32_t)h64, tag = state_tag(h64);
-    const uint32_t f = pr.f;
+    const uint32_t f = lane < kProbe ? ld_agent(c.flag + ((h + (uint32_t)lane) & c.mask)) : 0u;
     const uint64_t cand = __ballot(lane < kProbe && flag_ready(f) && flag_tag(f) == tag);
     const uint64_t empty = __ballot(lane < kProbe && f == 0u);
     if (!cand) return false;
@@ -967,8 +952,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             if (pa >= 0) s = next_state(s, pa);  // the leaf's state
             if (fail) break;
             levels += (unsigned int)(depth + 1);
-            // the cache probe's flags are requested first (a terminal leaf ignores them)
-            const CacheProbe probe = cache_probe_issue(cache, s);
             const bool lose = is_lose(s);
             const bool no_legal = legal_count(s) == 0u;
             clk.mark<kSpLeaf>();
@@ -1007,7 +990,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             const int k = min(tr.batch, tr.sims - sims_done);
             float *cv = s_hit[threadIdx.x >> 6];
             trips += cache.flag ? 1 : 0;
-            const bool hit = cache_lookup(cache, s, cv, probe);
+            const bool hit = cache_lookup(cache, s, cv);
             clk.mark<kSpProbe>();
             if (hit) {  // the flush's evaluation is already known: apply it now
                 trips += 4;
