@@ -1,0 +1,49 @@
+"""Launched by tests/test_dropins_gpu.py under torch.distributed.run with ONE rank and the nccl
+(RCCL) backend (not a test module): the RCCL branches of the data path and of data-parallel
+training on the real device. self_play_sharded's gather_records (device-tensor all_gather of the
+byte counts), broadcast_int, and DDP steps whose gradient all-reduce runs over RCCL. Two RCCL ranks
+cannot share one device, so this is the most of the 8-GPU path one GPU can run. Prints RCCL-OK."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "ultimate-tictactoe-alphazero_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+if __name__ == "__main__":
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl")
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    from oracle.hashnp import make_hash_model
+    from uttt_amd import SelfPlay
+    from uttt_amd.distributed import broadcast_int, self_play_sharded
+    from uttt_amd.model import random_network
+    from uttt_amd.train import train_step
+
+    n_games, seed = 6, 77
+    out = self_play_sharded(make_hash_model(), n_games, 3, seed, evaluate_count=20, batch_size=4)
+    sp = SelfPlay(3, 20, 4, 1.0)
+    sp.run(0, n_games, seed)
+    ref = sp.records()
+    assert len(out) == n_games, len(out)
+    for a, b in zip(sorted(out, key=lambda r: r["game"]), ref):
+        assert a["game"] == b["game"]
+        assert np.array_equal(np.asarray(a["actions"]), np.asarray(b["actions"]))
+        assert np.array_equal(np.asarray(a["policies"]).view(np.uint64), np.asarray(b["policies"]).view(np.uint64))
+        assert np.array_equal(np.asarray(a["values"]), np.asarray(b["values"]))
+    assert broadcast_int(123457) == 123457
+
+    net = random_network(0).cuda()
+    ddp = torch.nn.parallel.DistributedDataParallel(net, device_ids=[0], bucket_cap_mb=25)
+    opt = torch.optim.Adam(ddp.parameters(), lr=1e-3, fused=True)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = (torch.rand(16, 3, 9, 9, generator=g) > 0.5).float().cuda()
+    p = torch.softmax(torch.randn(16, 81, generator=g), 1).cuda()
+    v = (torch.rand(16, 1, generator=g) * 2 - 1).cuda()
+    losses = [float(train_step(ddp, opt, x, p, v)) for _ in range(3)]
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+    dist.destroy_process_group()
+    print("RCCL-OK", losses, flush=True)
