@@ -299,10 +299,13 @@ def summarize(r, steps):
     return out
 
 
-def conv_roofline(r):
+def conv_roofline(r, steps):
     """The dominant kernel: one residual-tower conv launch. achieved = executed MFMA flops per launch
     / the launch's average duration, from HIP events recorded on the lane's stream around each forward's
-    32 launches (so the few-us launch gaps are included: conservative)."""
+    32 launches (so the few-us launch gaps are included: conservative). Two lanes' launches overlap, so
+    that per-launch figure is not the kernel's share of the chip: chip_frac = every conv's executed flops
+    in the timed steps / the steps' wall time / peak, beside the per-step sum of conv launch time (which
+    exceeds ms_per_step by the overlap)."""
     conv = r["conv"]
     if not conv or not r["tower"]:
         return None
@@ -310,6 +313,7 @@ def conv_roofline(r):
     boards = sum(n for n, _ in r["tower"])
     ms = sum(t for _, t in r["tower"])
     launches = ncv * len(r["tower"])
+    chip_tflops = CONV_EXEC_FLOP[conv] * ncv * boards / r["elapsed"] / 1e12
     avg_us = ms * 1e3 / launches
     boards_per_launch = boards / len(r["tower"])
     flop = CONV_EXEC_FLOP[conv] * boards_per_launch
@@ -320,7 +324,13 @@ def conv_roofline(r):
     return {"kernel": f"k_{conv}_conv (residual-tower 3x3 conv, Winograd F(3x3,3x3) on the "
                       f"{'f16 MFMA, 3-term split-f16 products, f32 accumulation' if conv == 'wino3h' else 'f32 MFMA'})",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": CONV_PEAK[conv], "unit": "TFLOP/s",
-            "frac": round(achieved / CONV_PEAK[conv], 4), "traffic": traffic,
+            "frac": round(achieved / CONV_PEAK[conv], 4),
+            "chip_achieved": round(chip_tflops, 2), "chip_frac": round(chip_tflops / CONV_PEAK[conv], 4),
+            "conv_launch_ms_per_step": round(ms / steps, 3), "ms_per_step": round(r["elapsed"] / steps * 1e3, 3),
+            "frac_basis": "frac: per launch (HIP events around a forward's 32 launches on its lane's stream; the "
+                          "other lane's launches share the CUs meanwhile); chip_frac: all conv flops of the timed "
+                          "steps / their wall time (conv_launch_ms_per_step / ms_per_step = the lanes' overlap)",
+            "traffic": traffic,
             "traffic_detail": ({k: pmc[k] for k in ("hbm_bytes_per_board", "fetch_bytes_per_board_x2",
                                                     "write_bytes_per_board", "source") if k in pmc} if pmc else None),
             "algo_hbm_bytes_per_launch": round(algo_bytes),
@@ -517,7 +527,9 @@ def main():
                 sv["note"] = ("hash evaluator in place of the network: the search kernels' own rate, to set beside "
                               "cpu_baselines.b_tree_all_cores (the reference's C++ search with the same evaluator)")
             else:
-                sv["conv_roofline_frac"] = (conv_roofline(rv) or {}).get("frac")
+                cr = conv_roofline(rv, cfg["steps"]) or {}
+                sv["conv_roofline_frac"] = cr.get("frac")
+                sv["conv_chip_frac"] = cr.get("chip_frac")
             variants[key] = sv
 
     iso = None
@@ -571,7 +583,7 @@ def main():
                 "parallelism": f"games sharded over {world} GPU(s) by contiguous global-id blocks, "
                                f"no data-path collective",
             },
-            "roofline": conv_roofline(r) if conv else hbm_roofline("k_select", sel, r["trees_per_launch"],
+            "roofline": conv_roofline(r, args.steps) if conv else hbm_roofline("k_select", sel, r["trees_per_launch"],
                                                                    "pmc_select.json"),
             "roofline_select": dict(hbm_roofline("k_select (PUCT descent, one wave per tree)", sel,
                                                  r["trees_per_launch"], "pmc_select.json"),

@@ -39,6 +39,8 @@ extern "C" {
 #define UTTT_ERR_NONFINITE (-6) /* evaluator returned NaN/Inf (legal prior or value) */
 
 #define UTTT_ACTIONS 81
+#define UTTT_MAX_SIMS 4095 /* most simulations per search (uttt_engine_create max_sims): the 16-byte node
+                               record keeps N in 16 bits, k in 12, the first child in 20 */
 #define UTTT_INPUT_SIZE 243 /* (3, 9, 9) NCHW f32 per position */
 
 /* Packed, side-to-move-relative position (32 bytes; same bits on host and device).

@@ -170,6 +170,37 @@ def test_select_budget_changes_no_record(gpu, oracle_lib, budget, monkeypatch):
         assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64)), (budget, g)
 
 
+@pytest.mark.parametrize("depth", ["2", "3"])
+def test_round_lookahead_leaves_every_round_count_readable(gpu, oracle_lib, depth, monkeypatch):
+    """Rounds enqueued ahead of their count (UTTT_ROUND_LOOKAHEAD) and dropped when a lane's last game
+    ends, or when a move completes, get count 0: every RoundCount an evaluator saw is readable after
+    the run (round 4's bench crashed on one left unread), and the records still equal the oracle's."""
+    monkeypatch.setenv("UTTT_ROUND_LOOKAHEAD", depth)
+    n_games, seed = 10, 919
+    ref = [oracle_lib.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
+    seen = []
+
+    def make(eng):
+        inner = gpu.HashEvaluator(eng)
+
+        def ev(x, n):
+            seen.append(n)
+            return inner(x, n)
+        ev.device_count = True
+        ev.cheap = True
+        return ev
+
+    sp = gpu.SelfPlay(4, 30, 4, 1.0, lanes=2)
+    sp.set_evaluator(make)
+    sp.run(0, n_games, seed)
+    assert seen and all(int(n) >= 0 for n in seen)
+    recs = sp.records()
+    assert len(recs) == n_games
+    for g, r in enumerate(recs):
+        assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (depth, g)
+        assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64)), (depth, g)
+
+
 @pytest.mark.parametrize("tau", [0.0, 0.5, 2.0])
 def test_selfplay_other_temperatures_match_oracle(gpu, oracle_lib, tau):
     """k_move_end's one-hot (tau 0) and pow (tau != 1) score paths against the oracle's

@@ -125,6 +125,22 @@ def test_engine_limits_are_checked_before_the_device(engine_lib):
     assert engine_lib.uttt_engine_create(-1, 0, 50, ctypes.byref(h)) == -1
 
 
+def test_dropin_refuses_evaluate_count_above_the_node_record(uttt_cpp_mod):
+    """uttt_cpp.pv_mcts_scores with evaluate_count > UTTT_MAX_SIMS (4095) raises ValueError naming
+    the limit, before the model or the device is touched (the reference has no such bound;
+    INTEGRATION.md §2 'Limit')."""
+    called = []
+
+    def model(states):
+        called.append(len(states))
+        return [(np.zeros(81, np.float32), 0.0) for _ in states]
+
+    with pytest.raises(ValueError, match="4095"):
+        uttt_cpp_mod.pv_mcts_scores(model=model, state=uttt_cpp_mod.State(), temperature=1.0,
+                                    evaluate_count=4096, batch_size=8)
+    assert not called
+
+
 def test_calibrated_network_reproduces_reference_fixture():
     """tests/golden/netcal.npz pins the non-saturated network the GPU parity tests use: the
     seed-0 DualNetwork + the fixture's BatchNorm statistics (uttt_amd.model.calibrated_network)

@@ -120,7 +120,8 @@ struct Pool {
     uint4 *rec;
     int64_t cap;
 };
-constexpr int kMaxSimsRec = 4095;
+constexpr int kMaxSimsRec = UTTT_MAX_SIMS;
+static_assert(82 + 81ll * kMaxSimsRec < (1ll << 20), "first-child index: 20 bits");
 constexpr int kCountRing = 8;  // host-visible count slots per engine (uttt_search_select_async_to)
 
 struct Trees {

@@ -68,6 +68,15 @@ struct SearchEngine {
         if (eng) uttt_engine_destroy(eng);
     }
     uttt_engine_t *get(int sims) {
+        // The engine's 16-byte node record holds N, k and the first-child index in 16 / 12 / 20 bits
+        // (engine.hip, struct Pool): a tree of at most 4095 simulations. The reference has no such
+        // bound (uttt_mcts.cpp heap nodes); every caller in the reference uses 50 (self-play, arena)
+        // or 10 (test_cpp_mcts.py). Refused here, before any device work, with the reason.
+        if (sims > UTTT_MAX_SIMS)
+            throw py::value_error("pv_mcts_scores: evaluate_count " + std::to_string(sims) + " exceeds " +
+                                  std::to_string(UTTT_MAX_SIMS) +
+                                  ", the most simulations this engine's 16-byte node records hold per search "
+                                  "(INTEGRATION.md, limits)");
         if (!eng || sims > max_sims) {
             if (eng) uttt_engine_destroy(eng);
             eng = nullptr;

@@ -341,6 +341,11 @@ class SelfPlay:
                             ln.engine.apply(*ln.no_rows())
                 ln.spec = n > 0  # a round with leaves predicts another
                 if ln.cur_live == 0:  # every game of the lane is over: this move was empty
+                    # the rounds queued behind this one found no live tree either: their counts are 0
+                    # (left unread, a RoundCount raises when a caller later sizes a batch by it)
+                    for rc_empty, *_ in q:
+                        rc_empty.n = 0
+                    q.clear()
                     del state[key]
                     continue
                 if more > 0:  # some tree has simulations left once this round is applied
