@@ -45,5 +45,35 @@ if __name__ == "__main__":
     v = (torch.rand(16, 1, generator=g) * 2 - 1).cuda()
     losses = [float(train_step(ddp, opt, x, p, v)) for _ in range(3)]
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+
+    # round 5: the flat graphed data-parallel step (train.DPGraphedStep: graph(forward + backward into one
+    # flat gradient buffer) -> RCCL all_reduce of it -> graph(fused Adam)) against the eager DDP step on the
+    # same batches from the same weights: equal losses and weights (MIOpen immediate mode in both, so the
+    # same kernels; the tolerances cover Adam's first steps, whose update is ~lr * sign(g) per element)
+    from uttt_amd.train import DPGraphedStep
+    X = (torch.rand(64, 3, 9, 9, generator=g) > 0.5).float().cuda()
+    P = torch.softmax(torch.randn(64, 81, generator=g), 1).cuda()
+    V = (torch.rand(64, 1, generator=g) * 2 - 1).cuda()
+    idx = [torch.randperm(64, generator=g)[:16].cuda() for _ in range(3)]
+    net_a = random_network(0).cuda().train()
+    opt_a = torch.optim.Adam(net_a.parameters(), lr=torch.tensor(1e-3, device="cuda"), capturable=True, fused=True)
+    step = DPGraphedStep(net_a, opt_a, X, P, V, 16, 1.0, graph=True, tune=False)
+    net_b = random_network(0).cuda().train()
+    ddp_b = torch.nn.parallel.DistributedDataParallel(net_b, device_ids=[0], bucket_cap_mb=25)
+    opt_b = torch.optim.Adam(ddp_b.parameters(), lr=1e-3, fused=True)
+    la, lb = [], []
+    for i in idx:
+        step.loss_sum.zero_()
+        step.step(i, 1.0)
+        la.append(float(step.loss_sum))
+        lb.append(float(train_step(ddp_b, opt_b, X[i], P[i], V[i])))
+    assert abs(la[0] - lb[0]) <= 1e-5 * abs(lb[0]), (la, lb)
+    assert all(abs(a - b) <= 1e-3 * abs(b) for a, b in zip(la, lb)), (la, lb)
+    n_el = n_off = 0
+    for (k, qa), qb in zip(net_a.named_parameters(), net_b.parameters()):
+        d = (qa - qb).abs()
+        n_el += d.numel()
+        n_off += int((d > 1e-5).sum())
+    assert n_off <= 1e-4 * n_el, (n_off, n_el)
     dist.destroy_process_group()
-    print("RCCL-OK", losses, flush=True)
+    print("RCCL-OK", losses, "flat-graph DP", la, "eager DDP", lb, flush=True)

@@ -129,3 +129,65 @@ def test_data_parallel_step_equals_single_process(tmp_path):
     for k in m0["sd"]:
         assert torch.equal(m0["sd"][k], m1["sd"][k]), k
     assert m0["losses"] == m1["losses"] and all(np.isfinite(m0["losses"]))
+
+
+# ------------------------------- data-parallel step around one flat gradient all-reduce --
+def _flat_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from uttt_amd import train
+    from uttt_amd.model import random_network
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    # one step of DPGraphedStep's phases (eager form: graph A's body, the flat all-reduce, Adam) on an
+    # uneven split of a global batch of 7 (4 + 3 samples): BatchNorm on running statistics, so the
+    # per-sample losses and the reduced gradient equal the single-process ones up to summation order
+    model = random_network(0).eval()
+    x, p, v = (torch.from_numpy(a) for a in train.history_arrays(_history(7, 3)))
+    li = train.local_slice(torch.arange(7), rank, world)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    step = train.DPGraphedStep(model, opt, x, p, v, len(li), len(li) / 7, graph=False)
+    step.step(li, len(li) / 7)
+    if rank == 0:
+        torch.save({k: q.grad.clone() for k, q in model.named_parameters()}, os.path.join(out_dir, "g.pt"))
+    # train mode through train_network(dp="flat"): 21 plies in batches of 8 (the last one 5 = 3 + 2):
+    # parameters and the rank-averaged BatchNorm running statistics identical on both ranks
+    model2 = random_network(1)
+    losses = train.train_network(model2, _history(21, 5), epochs=2, batch_size=8, device=torch.device("cpu"),
+                                 log=None, dp="flat")
+    sd = {k: t.detach().clone() for k, t in model2.state_dict().items()}
+    torch.save({"sd": sd, "losses": losses}, os.path.join(out_dir, f"m{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_flat_data_parallel_step_equals_single_process(tmp_path):
+    """train.DPGraphedStep (round 5: the GPU data-parallel path's step as two graphs around one flat
+    gradient all-reduce), its phases run eagerly over 2 gloo ranks with an uneven split: the all-reduced
+    gradient equals the single-process gradient of the whole batch; train_network(dp="flat") keeps the
+    replicas' parameters and averaged BatchNorm statistics identical."""
+    import torch
+    from uttt_amd import train
+    from uttt_amd.model import random_network
+    mp.spawn(_flat_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    # the seed-0 network is saturated (near one-hot softmax), so f32 gradients carry ~2e-4 relative error
+    # against f64: the bound is the single-process f32 gradient's own distance from f64, doubled
+    x, p, v = (torch.from_numpy(a) for a in train.history_arrays(_history(7, 3)))
+    ref = {}
+    for dt in (torch.float32, torch.float64):
+        model = random_network(0).eval().to(dt)
+        pp, pv = model(x.to(dt))
+        loss = train.policy_loss_fn(pp, p.to(dt)) + torch.nn.functional.mse_loss(pv, v.to(dt))
+        loss.backward()
+        ref[dt] = {k: q.grad.double() for k, q in model.named_parameters()}
+    g = torch.load(os.path.join(tmp_path, "g.pt"), weights_only=True)
+    for k, g64 in ref[torch.float64].items():
+        scale = max(g64.abs().max().item(), 1e-12)
+        own = (ref[torch.float32][k] - g64).abs().max().item()
+        assert (g[k].double() - g64).abs().max().item() <= 2 * own + 1e-6 * scale, k
+    m0 = torch.load(os.path.join(tmp_path, "m0.pt"), weights_only=True)
+    m1 = torch.load(os.path.join(tmp_path, "m1.pt"), weights_only=True)
+    for k in m0["sd"]:
+        assert torch.equal(m0["sd"][k], m1["sd"][k]), k
+    assert m0["losses"] == m1["losses"] and all(np.isfinite(m0["losses"]))

@@ -156,6 +156,25 @@ def test_rccl_one_rank_data_path_and_ddp(gpu):
     assert "RCCL-OK" in r.stdout
 
 
+def test_flat_dp_train_network_two_ranks(gpu, tmp_path):
+    """train_network under torchrun on the GPU (its default data-parallel form, UTTT_TRAIN_DP=flat: the
+    per-rank step as two captured graphs around one flat gradient all-reduce), 2 ranks sharing the GPU over
+    gloo, different start weights per rank (rank 0's are broadcast): identical weights, averaged BatchNorm
+    running statistics and losses on both ranks (tests/dp_flat_two_ranks_main.py)."""
+    import torch
+    env = dict(os.environ, PYTHONPATH=REPO)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "tests", "dp_flat_two_ranks_main.py"), str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    m0 = torch.load(tmp_path / "m0.pt", weights_only=True)
+    m1 = torch.load(tmp_path / "m1.pt", weights_only=True)
+    for k in m0["sd"]:
+        assert torch.equal(m0["sd"][k], m1["sd"][k]), k
+    assert m0["losses"] == m1["losses"] and all(np.isfinite(m0["losses"]))
+
+
 def test_bench_multi_rank_path(gpu):
     """bench.py's N>1 path (what the driver's scaling run executes) rehearsed with 2 torchrun ranks
     on the one GPU (gloo instead of RCCL): per-rank game blocks, barrier + max-over-ranks timing,

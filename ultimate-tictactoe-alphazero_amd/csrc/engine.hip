@@ -20,6 +20,7 @@
 // Self-play (self_play_cpp.py) adds k_move_end (scores, f64 policy target,
 // numpy-legacy MT19937 choice, records), k_finalize (refill + arena offsets)
 // and k_archive.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1976,6 +1977,27 @@ struct TimedLaunch {
     }
 };
 
+// One kernel launch whose time the engine's telemetry keeps (round 5): with timing on, the start and
+// stop events are the dispatch's own (hipExtLaunchKernelGGL records them when the kernel starts and
+// completes, as rocprofv3's kernel trace measures it), not marker packets around the launch: a marker
+// pair added ~10 us per launch to the tree kernels (tree-only k_select 27.9 us under rocprofv3 against
+// 38.0 us between markers, k_apply 8.5 against 18.7; gpurun_out/t5a, profiles/r5/summary_tree_only.md).
+template <typename K, typename... Args>
+void timed_launch(uttt_engine *e, int kid, K kernel, dim3 grid, dim3 block, Args... args) {
+    e->launches[kid]++;
+    if (e->timing) {
+        hipEvent_t a = get_event(e), b = get_event(e);
+        if (a && b) {
+            hipExtLaunchKernelGGL(kernel, grid, block, 0, e->stream, a, b, 0, args...);
+            e->pending_ev.push_back({kid, a, b});
+            return;
+        }
+        if (a) e->ev_pool.push_back(a);
+        if (b) e->ev_pool.push_back(b);
+    }
+    hipLaunchKernelGGL(kernel, grid, block, 0, e->stream, args...);
+}
+
 // Fold finished event pairs into the totals (pairs whose end has not been reached yet, e.g.
 // behind the asynchronous rounds, stay pending).
 void drain_events(uttt_engine *e) {
@@ -2220,17 +2242,11 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     // leaf but some were stopped, select again (every launch completes >= 1 simulation
     // of each stopped tree, so this ends)
     for (;;) {
-        {
-            TimedLaunch tl(e, kKSelect);
-            hipLaunchKernelGGL(e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
-                               e->cache, e->timing ? e->d_bytes : nullptr);
-        }
+        timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)),
+                     dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
         if ((rc = check_launch())) return rc;
-        {
-            TimedLaunch tl(e, kKScan);
-            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr,
-                               (int32_t *)nullptr);
-        }
+        timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
+                     (int32_t *)nullptr);
         if ((rc = check_launch())) return rc;
         HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2239,9 +2255,8 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
         if (n > 0 || e->h_count[1] == 0) break;
     }
     if (n > 0 && nn_input) {
-        TimedLaunch tl(e, kKEncode);
         const int total = n * 243;
-        hipLaunchKernelGGL(k_encode, dim3((total + 255) / 256), dim3(256), 0, e->stream, e->tr, nn_input, n);
+        timed_launch(e, kKEncode, k_encode, dim3((total + 255) / 256), dim3(256), e->tr, nn_input, n);
     }
     if ((rc = check_launch())) return rc;
     e->n_pending = n;
@@ -2276,17 +2291,10 @@ static int select_async_impl(uttt_engine_t *e, int32_t *host_count) {
     }
     HIP_TRY(hipSetDevice(e->device));
     int rc = 0;
-    {
-        TimedLaunch tl(e, kKSelect);
-        hipLaunchKernelGGL(e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
-                           e->cache, e->timing ? e->d_bytes : nullptr);
-    }
+    timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)),
+                 dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
     if ((rc = check_launch())) return rc;
-    {
-        TimedLaunch tl(e, kKScan);
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, e->stream, e->tr, e->timing ? e->d_bytes : nullptr,
-                           host_count);
-    }
+    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count);
     if ((rc = check_launch())) return rc;
     e->n_pending = -1;
     e->phase = 3;
@@ -2383,10 +2391,9 @@ int uttt_search_apply(uttt_engine_t *e, const float *policy, int64_t pld, const 
         dvld = 1;
     }
     {
-        TimedLaunch tl(e, kKApply);
         EvalCache c = per_copy ? EvalCache{} : e->cache;  // the reference call pattern bypasses the cache
-        hipLaunchKernelGGL(k_apply, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, e->pool, e->tr, c, dp, dpld, dv, dvld,
-                           rowbase, per_copy ? 1 : 0, bytes_ptr(e, kKApply));
+        timed_launch(e, kKApply, k_apply, dim3(grid_waves(n)), dim3(kBlock), e->pool, e->tr, c, dp, dpld, dv, dvld,
+                     rowbase, per_copy ? 1 : 0, bytes_ptr(e, kKApply));
     }
     int rc = check_launch();
     if (rc) return rc;
@@ -2400,21 +2407,14 @@ int uttt_eval_hash(uttt_engine_t *e, const float *nn_input, int32_t n, float *po
     if (!e || !nn_input || !policy || !value || n < 0) return UTTT_ERR_ARG;
     if (n == 0) return UTTT_OK;
     HIP_TRY(hipSetDevice(e->device));
-    {
-        TimedLaunch tl(e, kKHash);
-        hipLaunchKernelGGL(k_hash_eval, dim3(grid_waves(n)), dim3(kBlock), 0, e->stream, nn_input, n, policy, value);
-    }
+    timed_launch(e, kKHash, k_hash_eval, dim3(grid_waves(n)), dim3(kBlock), nn_input, n, policy, value);
     return check_launch();
 }
 
 int uttt_eval_hash_dev(uttt_engine_t *e, float *policy, float *value) {
     if (!e || !policy || !value) return UTTT_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    {
-        TimedLaunch tl(e, kKHash);
-        hipLaunchKernelGGL(k_hash_leaves, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), 0, e->stream, e->tr, policy,
-                           value);
-    }
+    timed_launch(e, kKHash, k_hash_leaves, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), e->tr, policy, value);
     return check_launch();
 }
 

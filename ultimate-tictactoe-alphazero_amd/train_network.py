@@ -2,8 +2,10 @@
 load the newest ./data/*.history, train ./model/best.pth for RN_EPOCHS epochs
 (batch 128, Adam 1e-3, LambdaLR), save ./model/latest.pth. Run directly it
 trains on one GPU; under `torchrun --nproc-per-node N` (backend nccl = RCCL) it
-trains data-parallel over N GPUs with the same global batch
-(uttt_amd.train). The dataset is resident in HBM; no DataLoader workers.
+trains data-parallel over N GPUs with the same global batch (uttt_amd.train:
+per rank two captured graphs around one flat gradient all-reduce, per-rank
+BatchNorm statistics; UTTT_TRAIN_DP=ddp for eager DDP with SyncBatchNorm).
+The dataset is resident in HBM; no DataLoader workers.
 """
 import os
 import pickle
@@ -52,9 +54,8 @@ LAST_TIMINGS = {}
 def train_network():
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
     if distributed and not dist.is_initialized():
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        from uttt_amd.distributed import init_from_env
+        init_from_env()  # RCCL, one rank per GPU (gloo where ranks share a GPU)
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     LAST_TIMINGS.clear()
     t0 = time.perf_counter()

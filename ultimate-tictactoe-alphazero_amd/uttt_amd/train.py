@@ -186,6 +186,118 @@ class GraphedStep:
                 self._body(idx)
 
 
+class DPGraphedStep:
+    """The data-parallel step of a torchrun rank as two HIP graphs around ONE collective (round 5):
+
+      graph A: gather this rank's slice of the global batch from the HBM-resident dataset, forward,
+               loss x this rank's share of the global batch (n_r / N), backward into one flat
+               gradient buffer (every parameter's .grad is a view of it, so autograd accumulates in
+               place and nothing is copied);
+      all_reduce(SUM) of that buffer (RCCL over xGMI; 4.77 M f32 = 19.1 MB), enqueued on the current
+               stream between the replays: the averaged gradient of the global mean loss;
+      graph B: fused Adam (capturable, device-tensor learning rate).
+
+    ~600 kernel launches per step become two graph launches and one collective. DDP's bucketed
+    all-reduce overlaps the backward, but a captured graph cannot interleave host-issued collectives,
+    and the step at the per-rank batch of 16 is launch-bound, so one flat all-reduce
+    after the graph is the cheaper form. BatchNorm runs on each rank's own slice (per-rank batch
+    statistics, as plain DDP does): a numerics change against the reference's batch-128 statistics
+    (train_network.py:88-113 on one device), which SyncBatchNorm (UTTT_TRAIN_DP=ddp) keeps at ~70
+    small collectives per step. The running statistics are averaged over the ranks after every
+    epoch (train_network's caller sees one model on every rank).
+
+    graph=False runs the same three phases eagerly (the CPU / gloo form the multi-rank tests run)."""
+
+    def __init__(self, model, opt, x, p, v, local_batch, share, graph=True, tune=False):
+        """local_batch / share: this rank's slice of a full global batch and its n_r / N (the graphs')."""
+        self.model, self.opt, self.x, self.p, self.v = model, opt, x, p, v
+        self.rank, self.world = _world()
+        # the collective runs whenever a process group exists (one rank too: RCCL's path on one GPU)
+        self.collective = dist.is_available() and dist.is_initialized()
+        dev = x.device
+        params = [q for q in model.parameters() if q.requires_grad]
+        self.flat = torch.zeros(sum(q.numel() for q in params), device=dev)
+        o = 0
+        for q in params:  # .grad as views of one buffer: backward accumulates into it in place
+            q.grad = self.flat[o:o + q.numel()].view_as(q)
+            o += q.numel()
+        self.idx = torch.zeros(local_batch, dtype=torch.long, device=dev)
+        self.share_f = float(share)
+        self.share = torch.full((), self.share_f, device=dev)  # n_r / N of the static batch
+        self.loss_sum = torch.zeros((), device=dev)
+        self.graph = bool(graph) and dev.type == "cuda"
+        if not self.graph:
+            return
+        snap = {k: t.detach().clone() for k, t in model.state_dict().items()}
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        if tune:  # MIOpen's find on the current stream, outside any capture (as GraphedStep)
+            with torch.backends.cudnn.flags(enabled=True, benchmark=True, deterministic=False):
+                for _ in range(2):
+                    self._fb(self.idx, self.share)
+                    self.opt.step()
+            torch.cuda.synchronize(dev)
+        with torch.backends.cudnn.flags(enabled=True, benchmark=bool(tune), deterministic=False):
+            with torch.cuda.stream(side):
+                for _ in range(3):  # allocator, kernel choice, optimiser state
+                    self._fb(self.idx, self.share)
+                    self.opt.step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.g_fb, self.g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_fb):
+                self._fb(self.idx, self.share)
+            with torch.cuda.graph(self.g_opt, pool=self.g_fb.pool()):
+                self.opt.step()
+        with torch.no_grad():  # undo the warm-up: the graphs' tensors, the caller's values
+            for k, t in model.state_dict().items():
+                t.copy_(snap[k])
+            for st in opt.state.values():
+                for t in st.values():
+                    if torch.is_tensor(t):
+                        t.zero_()
+            self.flat.zero_()
+        self.loss_sum.zero_()
+
+    def _fb(self, idx, share):
+        self.flat.zero_()
+        if idx.numel():
+            pred_p, pred_v = self.model(self.x.index_select(0, idx))
+            loss = policy_loss_fn(pred_p, self.p.index_select(0, idx)) + \
+                nn.functional.mse_loss(pred_v, self.v.index_select(0, idx))
+            (loss * share).backward()
+            self.loss_sum += loss.detach() * share  # this rank's share of the global mean loss
+
+    def step(self, idx, share):
+        """One global-batch step: idx = this rank's slice (device tensor), share = its n_r / N."""
+        if self.graph and idx.numel() == self.idx.numel() and share == self.share_f:
+            self.idx.copy_(idx, non_blocking=True)
+            self.g_fb.replay()
+            if self.collective:
+                dist.all_reduce(self.flat)
+            self.g_opt.replay()
+            return
+        sh = torch.full((), float(share), device=self.flat.device)
+        with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=False):
+            self._fb(idx, sh)
+        if self.collective:
+            dist.all_reduce(self.flat)
+        self.opt.step()
+
+    def sync_buffers(self):
+        """Average the BatchNorm running statistics over the ranks (one all_reduce of a flat copy)."""
+        if self.world == 1:
+            return
+        bufs = [b for n, b in self.model.named_buffers() if n.endswith(("running_mean", "running_var"))]
+        flat = torch.cat([b.reshape(-1) for b in bufs])
+        dist.all_reduce(flat)
+        flat /= self.world
+        o = 0
+        with torch.no_grad():
+            for b in bufs:
+                b.copy_(flat[o:o + b.numel()].view_as(b))
+                o += b.numel()
+
+
 PRECISIONS = ("fp32", "f16")
 # "f16": convolutions and linear layers on f16 operands (10-bit mantissa, the reference's cuDNN TF32
 # default on its NVIDIA card has the same), f32 accumulation, BatchNorm / softmax / loss in f32
@@ -200,27 +312,39 @@ def _use_graph(graph, device, world):
 
 
 def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, device=None, seed=0, lr=0.001,
-                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=None, adam=None):
+                  log=print, sync_bn=None, graph=None, channels_last=False, precision=None, tune=None, adam=None,
+                  dp=None):
     """Train `model` (a DualNetwork) on `history` in place; returns the per-epoch mean losses.
     In a torch.distributed job every rank calls this with the same history and seed.
     graph (default on for one GPU; UTTT_TRAIN_GRAPH=0 disables): replay the step as a HIP graph
-    (GraphedStep); the eager loop otherwise (and for the data-parallel path)."""
+    (GraphedStep); the eager loop otherwise.
+    dp (UTTT_TRAIN_DP; data-parallel jobs only): "flat" (the default on GPUs) = DPGraphedStep, per-rank
+    BatchNorm statistics, two graphs around one flat gradient all-reduce; "ddp" (the default on the CPU)
+    = the eager DDP loop, with SyncBatchNorm on GPUs unless sync_bn=False (the reference's batch-128
+    statistics, ~70 small collectives per step)."""
+    import os
     rank, world = _world()
     device = device or (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
                         else torch.device("cpu"))
     x, p, v = (torch.from_numpy(a).to(device) for a in history_arrays(history))  # resident in HBM
     if precision is None:
-        import os
         precision = os.environ.get("UTTT_TRAIN_PRECISION", "fp32")
     if tune is None:  # MIOpen find before the capture (round 4: graph fp32 13.0k -> 16.3k samples/s)
-        import os
         tune = os.environ.get("UTTT_TRAIN_TUNE", "1") != "0"
     if adam is None:  # the graph step's Adam: "fused" (default) or "foreach" (rounds 1-3 for fp32)
-        import os
         adam = os.environ.get("UTTT_TRAIN_ADAM", "fused")
+    if dp is None:
+        dp = os.environ.get("UTTT_TRAIN_DP", "flat" if device.type == "cuda" else "ddp")
+    if dp not in ("flat", "ddp"):
+        raise ValueError("dp must be 'flat' or 'ddp'")
     if _use_graph(graph, device, world):
         return _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, channels_last, precision, tune,
                               adam)
+    if world > 1 and dp == "flat":
+        if precision != "fp32":
+            raise ValueError("the data-parallel step trains in fp32")
+        return _train_dp_flat(model, x, p, v, epochs, batch_size, device, seed, lr, log,
+                              graph=graph is not False and device.type == "cuda", tune=tune)
     if precision != "fp32":
         raise ValueError("precision other than fp32 needs the graph step (one GPU)")
     net = prepare(model, device, sync_bn)
@@ -246,6 +370,49 @@ def train_network(model, history, epochs=RN_EPOCHS, batch_size=BATCH_SIZE, devic
         losses.append(float(total) / nb)
         if log and rank == 0:
             log(f"Epoch {epoch + 1}/{epochs}, Loss: {losses[-1]:.4f}, LR: {sched.get_last_lr()[0]:.6f}")
+    return losses
+
+
+def _train_dp_flat(model, x, p, v, epochs, batch_size, device, seed, lr, log, graph=True, tune=False):
+    """The data-parallel loop on DPGraphedStep (see there): every rank draws the epoch's permutation from
+    the same generator and steps on its slice of each global batch."""
+    rank, world = _world()
+    net = model.to(device)
+    with torch.no_grad():  # one set of weights on every rank (DDP broadcasts rank 0's at construction)
+        for t in net.state_dict().values():
+            dist.broadcast(t, 0)
+    net.train()
+    if device.type == "cuda":
+        lr_t = torch.tensor(lr, dtype=torch.float32, device=device)
+        opt = torch.optim.Adam(net.parameters(), lr=lr_t, capturable=True, fused=True)
+    else:  # the reference's default Adam on the host
+        lr_t = None
+        opt = torch.optim.Adam(net.parameters(), lr=lr)
+    full = local_slice(torch.arange(batch_size), rank, world)
+    step = DPGraphedStep(net, opt, x, p, v, len(full), len(full) / batch_size, graph=graph, tune=tune)
+    losses = []
+    for epoch in range(epochs):
+        f = lr * lr_lambda(epoch)
+        if lr_t is not None:
+            lr_t.fill_(f)
+        else:
+            for g in opt.param_groups:
+                g["lr"] = f
+        step.loss_sum.zero_()
+        idxs = batches(len(x), batch_size, epoch, seed)
+        mine = [local_slice(b, rank, world) for b in idxs]
+        perm = torch.cat(mine).to(device, non_blocking=True)
+        o = 0
+        for b, li in zip(idxs, mine):
+            step.step(perm[o:o + len(li)], len(li) / len(b))
+            o += len(li)
+        total = step.loss_sum.clone()
+        if world > 1:
+            dist.all_reduce(total)
+        step.sync_buffers()
+        losses.append(float(total) / len(idxs))
+        if log and rank == 0:
+            log(f"Epoch {epoch + 1}/{epochs}, Loss: {losses[-1]:.4f}, LR: {lr * lr_lambda(epoch + 1):.6f}")
     return losses
 
 
@@ -285,5 +452,5 @@ def _train_graphed(model, x, p, v, epochs, batch_size, device, seed, lr, log, ch
     return losses
 
 
-__all__ = ["BATCH_SIZE", "F16_LOSS_SCALE", "GraphedStep", "PRECISIONS", "RN_EPOCHS", "batches", "history_arrays", "local_slice", "lr_lambda",
+__all__ = ["BATCH_SIZE", "DPGraphedStep", "F16_LOSS_SCALE", "GraphedStep", "PRECISIONS", "RN_EPOCHS", "batches", "history_arrays", "local_slice", "lr_lambda",
            "policy_loss_fn", "prepare", "train_network", "train_step"]
