@@ -248,7 +248,9 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
         timed_eval.device_count = getattr(inner, "device_count", False)
         return timed_eval
 
-    sp.set_evaluator(make_timed)
+    # the hash evaluator runs inside the engine's one-call rounds (Engine.round_hash_async): no per-round
+    # Python evaluator call to wrap; its time is the engine's own dispatch-event telemetry ("hash_eval")
+    sp.set_evaluator(HashEvaluator if evaluator == "hash" else make_timed)
     # continuous self-play: rank r owns the contiguous block r of global game ids (the same
     # scheme as self_play_cpp's torchrun sharding), large enough for every game it can start
     per_rank = (age + warmup + steps + 2) * games
@@ -261,7 +263,7 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     rows.clear()
     sp.reset_stats()
     sp.set_timing(True)
-    rounds0, finished0 = sp.rounds, sp.finished
+    rounds0, finished0, leaves0 = sp.rounds, sp.finished, sp.leaves
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -278,9 +280,13 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     # rounds enqueued before their count was known may have had no leaf (the move's last select)
     tower = [(int(n), a.elapsed_time(b)) for n, a, b in tower_events if int(n) > 0]
     st = {k: sp.kernel_stats(k) for k in ("select", "apply", "scan", "move_end", "select_levels", "select_trees",
-                                          "select_max_levels_sum", "select_trips", "select_max_trips_sum")}
-    out = {"sims": done, "elapsed": elapsed, "rows": sum(int(n) for n in rows), "nn_ms": union_ms(ivs),
-           "nn_lane_sum_ms": sum(hi - lo for lo, hi in ivs), "tower": tower, "stats": st,
+                                          "select_max_levels_sum", "select_trips", "select_max_trips_sum", "hash_eval")}
+    if evaluator == "hash":
+        n_rows, nn_ms, nn_sum = sp.leaves - leaves0, st["hash_eval"]["ms"], st["hash_eval"]["ms"]
+    else:
+        n_rows, nn_ms, nn_sum = sum(int(n) for n in rows), union_ms(ivs), sum(hi - lo for lo, hi in ivs)
+    out = {"sims": done, "elapsed": elapsed, "rows": n_rows, "nn_ms": nn_ms,
+           "nn_lane_sum_ms": nn_sum, "tower": tower, "stats": st,
            "rounds": sp.rounds - rounds0, "finished": sp.finished - finished0, "conv": conv,
            "cache": sp.cache_stats() if cache_log2 else None, "trees_per_launch": games // lanes}
     del sp
@@ -428,17 +434,63 @@ def chase_latency(chase):
     return None
 
 
-def hbm_roofline(name, stat, trees_per_launch, pmc_name=None):
+def fetch_factor():
+    """FETCH_SIZE correction for the tree kernels' reads, measured on their own load shapes
+    (tools/diag/fetch_cal.hip at k_select's concurrency, profiles/r*/fetch_cal.json): FETCH_SIZE counts 64 B
+    per L2 read request whatever its size, so 16-B-per-lane loads of L consecutive 16-B records (a child-scan
+    group; L uniform over 1..64) read 1/0.554 of what it reports, full 1-KB groups 2x, and a lone 16-B
+    record 1/4 of it."""
+    cal = newest_profile("fetch_cal.json", {})
+    if not cal:
+        return None
+    sh = cal["shapes"]
+    return {"factor": sh["partial_group_Lx16B"]["correction_factor"], "shape": "partial_group_Lx16B",
+            "bounds": [sh["single_record_16B"]["correction_factor"], sh["group64_dwordx4_1KB"]["correction_factor"]],
+            "source": cal["source"]}
+
+
+def hbm_roofline(name, stat, trees_per_launch, pmc_name=None, evaluator=None, sims=None):
+    """A tree kernel against HBM. achieved = algorithmic bytes per launch of THIS run / the kernel's rocprof
+    average duration from the committed kernel trace of the same command (profiles/r*/prof_*.json, matched
+    on evaluator, trees per launch and sims; BASELINE.md §3 'algorithmic bytes / rocprof time'), or the
+    dispatch events' average where no such trace is committed. The engine times each launch by its own
+    dispatch's events (hipExtLaunchKernelGGL); they still run ~5 us over rocprof per launch, both figures are
+    kept. traffic = PMC reads x the FETCH_SIZE factor measured on the kernels' load shape + writes."""
     ms, launches, byts = stat["ms"], max(stat["launches"], 1), stat["bytes"]
-    achieved = (byts / 1e9) / (ms / 1e3) if ms > 0 else 0.0
+    ev_us = ms * 1e3 / launches
+    kname = name.split()[0]
+    prof = None
+    if evaluator is not None:
+        for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "prof_*.json")), reverse=True):
+            with open(f) as fh:
+                d = json.load(fh)
+            if (d.get("evaluator") == evaluator and d.get("trees_per_launch") == trees_per_launch
+                    and d.get("sims_per_move") == sims and any(c["kernel"] == kname for c in d["checks"].values())):
+                prof = d
+                prof["source"] = os.path.relpath(f, REPO)
+                break
+    rp_us = None
+    if prof:
+        rp_us = next(c["rocprof_avg_us"] for c in prof["checks"].values() if c["kernel"] == kname)
+    us = rp_us if rp_us else ev_us
+    achieved = (byts / launches / 1e9) / (us * 1e-6) if us > 0 else 0.0
     pmc = newest_profile(pmc_name, {"trees_per_launch": trees_per_launch}) if pmc_name else None
+    ff = fetch_factor()
+    traffic, detail = None, None
+    if pmc:
+        k = ff["factor"] if ff else 1.0
+        traffic = round(pmc["fetch_bytes"] * k + pmc["write_bytes"])
+        detail = {"read_bytes_fetch_size": round(pmc["fetch_bytes"]), "write_bytes": round(pmc["write_bytes"]),
+                  "read_correction": ff, "traffic_bounds": ([round(pmc["fetch_bytes"] * b + pmc["write_bytes"])
+                                                             for b in ff["bounds"]] if ff else None),
+                  "source": pmc["source"]}
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": round(pmc["traffic_bytes_raw"]) if pmc else None,
-            "traffic_detail": ({"read_bytes": round(pmc["fetch_bytes"]), "write_bytes": round(pmc["write_bytes"]),
-                                "source": pmc["source"]} if pmc else None),
-            "algo_bytes_per_launch": round(byts / launches), "avg_launch_us": round(ms * 1e3 / launches, 2),
-            "launches": stat["launches"]}
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_detail": detail,
+            "algo_bytes_per_launch": round(byts / launches), "avg_launch_us": round(us, 2),
+            "avg_launch_us_basis": ("rocprof kernel trace of the same command: " + prof["source"]) if prof else
+                                   "dispatch events of this run",
+            "rocprof_avg_launch_us": round(rp_us, 2) if rp_us else None,
+            "event_avg_launch_us": round(ev_us, 2), "launches": stat["launches"]}
 
 
 def main():
@@ -518,9 +570,11 @@ def main():
             if cfg["evaluator"] == "hash":
                 sv["net"] = None
                 sv["roofline_select"] = hbm_roofline("k_select", rv["stats"]["select"], rv["trees_per_launch"],
-                                                     "pmc_select_tree.json" if cfg["sims"] == S else None)
+                                                     "pmc_select_tree.json" if cfg["sims"] == S else None,
+                                                     "hash", cfg["sims"])
                 sv["roofline_backup"] = hbm_roofline("k_apply", rv["stats"]["apply"], rv["trees_per_launch"],
-                                                     "pmc_apply_tree.json" if cfg["sims"] == S else None)
+                                                     "pmc_apply_tree.json" if cfg["sims"] == S else None,
+                                                     "hash", cfg["sims"])
                 sv["breakdown_ms"] = {k: round(rv["stats"][k]["ms"], 2) for k in ("select", "apply", "scan", "move_end")}
                 sv["breakdown_ms"]["evaluator"] = round(rv["nn_ms"], 2)
                 sv["breakdown_ms"]["wall"] = round(rv["elapsed"] * 1e3, 2)
@@ -551,6 +605,9 @@ def main():
         max_trips = st["select_max_trips_sum"]["bytes"] / sel_launches
         sel_us = sel["ms"] * 1e3 / sel_launches
         chase_lat = chase_latency(newest_profile("chase.json", {}))
+        tree = args.evaluator == "hash"
+        pmc_sel = "pmc_select_tree.json" if tree else "pmc_select.json"
+        pmc_app = "pmc_apply_tree.json" if tree else "pmc_apply.json"
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -584,9 +641,9 @@ def main():
                                f"no data-path collective",
             },
             "roofline": conv_roofline(r, args.steps) if conv else hbm_roofline("k_select", sel, r["trees_per_launch"],
-                                                                   "pmc_select.json"),
+                                                                   pmc_sel, args.evaluator, S),
             "roofline_select": dict(hbm_roofline("k_select (PUCT descent, one wave per tree)", sel,
-                                                 r["trees_per_launch"], "pmc_select.json"),
+                                                 r["trees_per_launch"], pmc_sel, args.evaluator, S),
                                     latency_model={
                                         "levels_per_tree_per_launch": round(st["select_levels"]["bytes"] / lev_trees, 2),
                                         "slowest_tree_levels_per_launch": round(max_lev, 1),
@@ -604,7 +661,7 @@ def main():
                                                 "the dependent-load latency of tools/diag/chase.hip (2,048 waves, "
                                                 "random 256-B loads that miss L2)"}),
             "roofline_backup": hbm_roofline("k_apply (expand + backup, one wave per pending leaf)", st["apply"],
-                                            r["trees_per_launch"], "pmc_apply.json"),
+                                            r["trees_per_launch"], pmc_app, args.evaluator, S),
             "nn": {"rows_evaluated": r["rows"], "ms": round(r["nn_ms"], 2),
                    "share_of_step": round(r["nn_ms"] / 1e3 / r["elapsed"], 4),
                    "lane_sum_ms": round(r["nn_lane_sum_ms"], 2),

@@ -177,6 +177,15 @@ int uttt_eval_hash(uttt_engine_t *eng, const float *nn_input, int32_t n, float *
 /* The same evaluator on the round's pending leaves read from their states, the count read on the
  * device (after uttt_search_select_async): rows [0, count) of policy (81 f32 each) and value. */
 int uttt_eval_hash_dev(uttt_engine_t *eng, float *policy, float *value);
+/* One whole round with the hash evaluator, enqueued by one call (round 5; the rounds of
+ * SelfPlay.steps with HashEvaluator lanes, i.e. the kernel microbenchmark of SURVEY §8(d)):
+ * uttt_search_select_async_to(ring_slot) -> uttt_eval_hash_dev(policy, value) ->
+ * uttt_search_apply(on_device). The scan stores the round's counts and then `tag` (word 3 of the
+ * slot, a system-scope release store), so the host learns that the counts landed by polling the
+ * tag: no event and no host sync per round. policy: (max_trees, 81) f32, value: (max_trees,) f32,
+ * device memory. Replaces, for the test evaluator, one pass of the flush loop of
+ * uttt_mcts.cpp:109-167 over every tree. */
+int uttt_round_hash_async(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, float *policy, float *value);
 
 /* Root results after the search: visit counts of the root's children (legal
  * order, row stride 81) and |legal| per tree. */

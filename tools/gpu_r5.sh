@@ -23,6 +23,9 @@ for s in $STEPS; do
                > $OUT/gputests.log 2>&1 ;;
     smoke) timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     ring)  timeout -k 10 120 tools/diag/lds_ring ${RING_CHUNKS:-64} > $OUT/lds_ring.json 2> $OUT/lds_ring.log ;;
+    gemm)  timeout -k 10 180 tools/diag/gemm_phase ${GEMM_CHUNKS:-64} > $OUT/gemm_phase.json 2> $OUT/gemm_phase.log ;;
+    counters) timeout -k 10 120 rocprofv3 -L > $OUT/counters_all.txt 2> $OUT/counters.log; \
+           grep -E "TCC_EA0_RD|TCC_REQ|TCC_READ|TCC_BUBBLE|TCC_EA0_WR" $OUT/counters_all.txt > $OUT/counters_tcc.txt; true ;;
     fcal)  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fcal1 -o f \
                -- tools/diag/fetch_cal > $OUT/fetch_cal.json 2> $OUT/fcal1.log && \
            timeout -s KILL 90 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
@@ -34,11 +37,11 @@ for s in $STEPS; do
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated --evaluator hash --lanes 1 --age 100 \
                --steps 20 --warmup 3 > $OUT/tprof_bench.log 2>&1 && \
            python3 tools/prof_summary.py $(ls $OUT/tprof/*/bench_kernel_trace.csv $OUT/tprof/bench_kernel_trace.csv 2>/dev/null | head -1) \
-               $OUT/tprof_bench.log $OUT/summary_tree_only.md > $OUT/tprof_summary.log 2>&1 ;;
+               $OUT/tprof_bench.log $OUT/prof_tree_only.md > $OUT/tprof_summary.log 2>&1 ;;
     hprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/hprof -o bench \
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/hprof_bench.log 2>&1 && \
            python3 tools/prof_summary.py $(ls $OUT/hprof/*/bench_kernel_trace.csv $OUT/hprof/bench_kernel_trace.csv 2>/dev/null | head -1) \
-               $OUT/hprof_bench.log $OUT/summary.md > $OUT/hprof_summary.log 2>&1 ;;
+               $OUT/hprof_bench.log $OUT/prof_headline.md > $OUT/hprof_summary.log 2>&1 ;;
     pmctree) PMC_OUT=$OUT/pmc_tree PMC_AGE=100 PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
                > $OUT/pmc_tree.log 2>&1 && \
              python tools/pmc_summary.py $OUT/pmc_tree $OUT/pmc_tree/p1.log $OUT/pmc_select_tree.json k_select >> $OUT/pmc_tree.log && \

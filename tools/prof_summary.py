@@ -67,6 +67,29 @@ def main(trace, bench_log, out):
     with open(out, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
+    # the same window as JSON beside the .md: bench.py reads the rocprof averages of the tree kernels from it
+    # (newest_profile), matched to its own configuration
+    cfg = bench["config"]
+    js = {"trace": trace, "bench_log": bench_log, "bench_value": bench["value"],
+          "evaluator": ("hash" if "hash" in cfg.get("evaluator", "") else
+                        "fused" if "HIP kernels" in cfg.get("evaluator", "") else "nn"),
+          "games_per_gpu": cfg.get("games_per_gpu"),
+          "sims_per_move": cfg.get("sims_per_move"), "lanes_per_gpu": cfg.get("lanes_per_gpu"),
+          "trees_per_launch": cfg.get("games_per_gpu", 0) // max(cfg.get("lanes_per_gpu", 1), 1),
+          "window_dispatches_k_select": nwin, "span_ms": span / 1e6, "busy_ms": total / 1e6,
+          "kernels": {n: {"calls": a[0], "avg_us": a[1] / a[0] / 1e3, "total_ms": a[1] / 1e6} for n, a in agg.items()},
+          "checks": {}}
+    for key in ("roofline", "roofline_select", "roofline_backup"):
+        rf = bench.get(key)
+        if not rf:
+            continue
+        kname = rf["kernel"].split()[0]
+        sw = [r for r in win if kname in r[2]]
+        js["checks"][key] = {"kernel": kname, "rocprof_avg_us": sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3,
+                             "rocprof_dispatches": len(sw), "event_avg_us": rf["avg_launch_us"],
+                             "event_launches": rf["launches"]}
+    with open(out.rsplit(".", 1)[0] + ".json", "w") as f:
+        json.dump(js, f, indent=1)
 
 
 if __name__ == "__main__":

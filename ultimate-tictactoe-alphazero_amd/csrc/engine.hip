@@ -1097,8 +1097,10 @@ __device__ __forceinline__ T block_scan_1024(T v, T *total, T *wsum /* __shared_
 // One block: exclusive scan of pending flags -> tree_of[slot] in tree order.
 // host_count (optional): the three counts are also stored to this host-visible (fine-grained pinned)
 // word triple at system scope, so the host reads a round's counts when the round's event completes
-// without a copy operation on the stream (round 4: one stream operation less per round)
-__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count) {
+// without a copy operation on the stream (round 4: one stream operation less per round). Round 5: word 3
+// gets the round's tag after them (a system-scope release store), so a host that polls the tag needs no
+// event either (uttt_round_hash_async).
+__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count, int32_t tag) {
     __shared__ unsigned long long wsum[16];
     const int tid = threadIdx.x;
     if (stats && tid < 64) {  // the select launch before this scan is complete: fold its slowest tree
@@ -1153,6 +1155,7 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
             __hip_atomic_store(host_count + 0, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 1, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 2, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_count + 3, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -2246,7 +2249,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
                      dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
         if ((rc = check_launch())) return rc;
         timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
-                     (int32_t *)nullptr);
+                     (int32_t *)nullptr, (int32_t)0);
         if ((rc = check_launch())) return rc;
         HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2265,7 +2268,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     return UTTT_OK;
 }
 
-static int select_async_impl(uttt_engine_t *e, int32_t *host_count);
+static int select_async_impl(uttt_engine_t *e, int32_t *host_count, int32_t tag = 0);
 int uttt_search_select_async(uttt_engine_t *e) { return select_async_impl(e, nullptr); }
 
 int uttt_search_select_async_to(uttt_engine_t *e, int32_t ring_slot) {
@@ -2283,7 +2286,7 @@ int uttt_search_count_ring(uttt_engine_t *e, const int32_t **ring, int32_t *n_sl
     return UTTT_OK;
 }
 
-static int select_async_impl(uttt_engine_t *e, int32_t *host_count) {
+static int select_async_impl(uttt_engine_t *e, int32_t *host_count, int32_t tag) {
     if (!e) return UTTT_ERR_ARG;
     if (e->phase != 1) {
         set_error("uttt_search_select_async: call uttt_search_begin (or apply the previous round) first");
@@ -2294,7 +2297,7 @@ static int select_async_impl(uttt_engine_t *e, int32_t *host_count) {
     timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)),
                  dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
     if ((rc = check_launch())) return rc;
-    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count);
+    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count, tag);
     if ((rc = check_launch())) return rc;
     e->n_pending = -1;
     e->phase = 3;
@@ -2416,6 +2419,17 @@ int uttt_eval_hash_dev(uttt_engine_t *e, float *policy, float *value) {
     HIP_TRY(hipSetDevice(e->device));
     timed_launch(e, kKHash, k_hash_leaves, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), e->tr, policy, value);
     return check_launch();
+}
+
+int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value) {
+    if (!e || !policy || !value || ring_slot < 0 || ring_slot >= kCountRing) {
+        set_error("uttt_round_hash_async: bad arguments (ring slot must be in 0..%d)", kCountRing - 1);
+        return UTTT_ERR_ARG;
+    }
+    int rc = select_async_impl(e, e->h_ring + 4 * ring_slot, tag);
+    if (rc) return rc;
+    if ((rc = uttt_eval_hash_dev(e, policy, value))) return rc;
+    return uttt_search_apply(e, policy, 81, value, 1, 0, 1);
 }
 
 static int check_tree_errors(uttt_engine *e) {

@@ -62,14 +62,14 @@ constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS lat
 constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
 constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
-constexpr int kFoldAT = 1 << 18;
+constexpr int kFoldAT = 1 << 18;          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
 constexpr int kEpiBarrier = 1 << 7;       // a set's epilogue starts after every wave's last point GEMMs (a barrier):
                                           // the earlier waves' epilogue VALU no longer takes the issue slots of
                                           // their SIMD partners' last point GEMMs
 constexpr int kEpiPrio = 1 << 10;         // ... instead: waves 4-7 run a set's last point loop at s_setprio 1
 constexpr int kEarlyLoad = 1 << 19;       // the chunk-after-next's inputs requested at the end of this chunk's
                                           // point GEMMs (before the barrier the earlier waves wait at), except
-                                          // after a set's last chunk (its epilogue needs the registers)          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
+                                          // after a set's last chunk (its epilogue needs the registers)
 constexpr int kStagger = 1 << 30;         // waves 4-7 walk the 25 points from kStaggerRot on (their SIMD partners
                                           // from 0), so the partners' fold-free and fold-heavy points interleave
 constexpr int kStaggerRot = 12;

@@ -175,6 +175,16 @@ class Engine:
         check(self.lib.uttt_eval_hash_dev(self.h, ctypes.c_void_p(policy.data_ptr()),
                                           ctypes.c_void_p(value.data_ptr())))
 
+    def round_hash_async(self, ring_slot, policy, value):
+        """A whole round with the hash evaluator in one call (uttt_round_hash_async): select, scan (the counts
+        and then a new tag into ring slot ring_slot), hash evaluation of the pending leaves, apply. Returns
+        the tag; the round's counts in count_ring()[ring_slot] are valid once its word 3 equals it."""
+        self.tag = getattr(self, "tag", 0) + 1
+        check(self.lib.uttt_round_hash_async(self.h, int(ring_slot), self.tag, ctypes.c_void_p(policy.data_ptr()),
+                                             ctypes.c_void_p(value.data_ptr())))
+        self.n_pending = None
+        return self.tag
+
     def eval_hash(self, nn_input, n, policy, value):
         check(self.lib.uttt_eval_hash(self.h, ctypes.c_void_p(nn_input.data_ptr()), int(n),
                                       ctypes.c_void_p(policy.data_ptr()), ctypes.c_void_p(value.data_ptr())))

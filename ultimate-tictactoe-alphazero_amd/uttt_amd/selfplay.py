@@ -47,6 +47,11 @@ class HashEvaluator:
         self.engine.eval_hash(x, n, self.policy, self.value)
         return self.policy[:n], self.value[:n]
 
+    def round_async(self, engine, slot):
+        """The whole round in one C call (Engine.round_hash_async: select, scan, this evaluator, apply);
+        SelfPlay.steps then polls the returned tag in the host count ring instead of an event."""
+        return engine.round_hash_async(slot, self.policy, self.value)
+
 
 class NetworkEvaluator:
     """DualNetwork (or any model with its call signature) on the engine's device."""
@@ -103,6 +108,18 @@ class BatchedSearch:
         return self.engine.root_visits()
 
 
+class _TagReady:
+    """Readiness of a one-call round: its ring slot's word 3 holds the round's tag (stored by k_scan after
+    the counts, a system-scope release), polled like an event."""
+    __slots__ = ("buf", "tag")
+
+    def __init__(self, buf, tag):
+        self.buf, self.tag = buf, tag
+
+    def query(self):
+        return int(self.buf[3]) == self.tag
+
+
 class _Lane:
     """One engine + its stream, input buffer and evaluator."""
 
@@ -122,6 +139,7 @@ class _Lane:
         self.ring_pos = 0
         self.spec = True        # enqueue the next round's network before its count is known
         self._no_rows = None
+        self.leaves = 0         # pending leaves of this lane's rounds (the rows its evaluator was asked for)
 
     def no_rows(self):
         """(policy, value) device buffers for an apply with no pending leaf (nothing is read)."""
@@ -206,6 +224,11 @@ class SelfPlay:
     @property
     def finished(self):
         return sum(ln.finished for ln in self.lanes)
+
+    @property
+    def leaves(self):
+        """Pending leaves of all rounds the device-count loop (steps) read back."""
+        return sum(ln.leaves for ln in self.lanes)
 
     def _ctx(self, ln):
         return torch.cuda.stream(ln.stream) if ln.stream is not None else contextlib.nullcontext()
@@ -330,6 +353,7 @@ class SelfPlay:
                         progress(self.finished, None)
                 n, more = int(buf[0]), int(buf[2])
                 rc.n = n
+                ln.leaves += n
                 if n > 0:
                     ln.rounds += 1
                 if not spec:  # the network was held back until the count was known
@@ -402,6 +426,11 @@ class SelfPlay:
         slot = ln.ring_pos % len(ln.count_ring)
         buf = ln.count_ring[slot]
         ln.ring_pos += 1
+        one_call = getattr(ln.evaluator, "round_async", None)
+        if spec and one_call is not None:
+            # the whole round in one C call, on the engine's stream; readiness is the tag the scan stores
+            # into the ring slot after the counts (no event, no torch stream context per round)
+            return rc, _TagReady(buf, one_call(ln.engine, slot)), spec, buf
         with self._ctx(ln):
             ln.engine.select_async_to(slot)
             ev = torch.cuda.Event()
