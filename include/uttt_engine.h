@@ -161,6 +161,14 @@ int uttt_search_count_ring(uttt_engine_t *eng, const int32_t **ring, int32_t *n_
 /* Host copies of the pending leaves (slot order) and their multiplicity k
  * (the number of identical copies the reference would have queued). */
 int uttt_search_pending(uttt_engine_t *eng, uttt_state_t *states, int32_t *copies);
+/* One-tree searches (the drop-in uttt_cpp.pv_mcts_scores, python_bindings.cpp:83-100 / uttt_mcts.cpp:109-167)
+ * without a copy operation or a stream synchronisation per flush (round 5): select_host launches the
+ * select and the scan, which stores the counts, the pending leaf's state and its copies k into fine-grained
+ * pinned host memory and then a tag the host spins on; apply_host copies the leaf's evaluation (81 priors
+ * by action, value) into pinned host memory that k_apply reads directly, and returns without waiting.
+ * Same results as uttt_search_select + uttt_search_pending + uttt_search_apply (one result per leaf). */
+int uttt_search_select_host(uttt_engine_t *eng, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending);
+int uttt_search_apply_host(uttt_engine_t *eng, const float *policy81, float value);
 
 /* Evaluator results for the pending leaves (uttt_mcts.cpp:138-167: legal-mask,
  * sequential f32 renormalisation, expand k times, back up k times).

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -108,6 +109,16 @@ struct LeafRec {
     int32_t depth;
     int32_t k;
     int32_t pad;
+};
+
+// A single-tree search's round result in fine-grained pinned host memory (round 5, uttt_search_select_host):
+// k_scan stores the counts, the pending leaf's state and its copies, then the tag (a system-scope release),
+// and the host polls the tag: one select per flush costs no copy operation and no stream synchronisation
+// (the reference's flush loop, uttt_mcts.cpp:109-167, runs in-process).
+struct HostLeaf {
+    int32_t count, stopped, left, tag;
+    int32_t k, pad0, pad1, pad2;
+    uttt_state_t state;
 };
 
 // One node (round 4: four SoA arrays N, W, P, LINK became one record, so the PUCT scan loads a child
@@ -1100,7 +1111,8 @@ __device__ __forceinline__ T block_scan_1024(T v, T *total, T *wsum /* __shared_
 // without a copy operation on the stream (round 4: one stream operation less per round). Round 5: word 3
 // gets the round's tag after them (a system-scope release store), so a host that polls the tag needs no
 // event either (uttt_round_hash_async).
-__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count, int32_t tag) {
+__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count, int32_t tag,
+                                               HostLeaf *host_leaf) {
     __shared__ unsigned long long wsum[16];
     const int tid = threadIdx.x;
     if (stats && tid < 64) {  // the select launch before this scan is complete: fold its slowest tree
@@ -1156,6 +1168,20 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
             __hip_atomic_store(host_count + 1, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 2, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 3, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (host_leaf) {  // a one-tree engine: tree 0 is slot 0's
+            __hip_atomic_store(&host_leaf->count, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_leaf->stopped, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_leaf->left, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (c0 > 0) {
+                const uttt_state_t st = tr.leaf[0];
+                const int32_t *w = reinterpret_cast<const int32_t *>(&st);
+                int32_t *d = reinterpret_cast<int32_t *>(&host_leaf->state);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&host_leaf->k, tr.rec[0].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __hip_atomic_store(&host_leaf->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -1887,7 +1913,10 @@ struct uttt_engine {
     Pool pool{};
     Trees tr{};
     int32_t *h_count = nullptr;  // pinned
-    int32_t *h_ring = nullptr;   // fine-grained pinned: kCountRing x {pending, stopped, left, pad}, k_scan-written
+    int32_t *h_ring = nullptr;   // fine-grained pinned: kCountRing x {pending, stopped, left, tag}, k_scan-written
+    HostLeaf *h_leaf = nullptr;  // fine-grained pinned: a one-tree round's result (uttt_search_select_host)
+    float *h_eval = nullptr;     // fine-grained pinned: its evaluation, read by k_apply (uttt_search_apply_host)
+    int32_t leaf_tag = 0;
     int32_t *d_rowbase = nullptr;
     float *d_pol_scratch = nullptr;
     float *d_val_scratch = nullptr;
@@ -2132,6 +2161,13 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         return fail(UTTT_ERR_HIP);
     }
     memset(e->h_ring, 0, sizeof(int32_t) * 4 * kCountRing);
+    if (hipHostMalloc((void **)&e->h_leaf, sizeof(HostLeaf), hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc((void **)&e->h_eval, sizeof(float) * 96, hipHostMallocCoherent) != hipSuccess) {
+        set_error("hipHostMalloc failed");
+        return fail(UTTT_ERR_HIP);
+    }
+    memset(e->h_leaf, 0, sizeof(HostLeaf));
+    memset(e->h_eval, 0, sizeof(float) * 96);
     if (hipHostMalloc((void **)&e->h_count, sizeof(int32_t) * 4, hipHostMallocDefault) != hipSuccess) {
         set_error("hipHostMalloc failed");
         return fail(UTTT_ERR_HIP);
@@ -2164,6 +2200,8 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     }
     if (e->h_count) (void)hipHostFree(e->h_count);
     if (e->h_ring) (void)hipHostFree(e->h_ring);
+    if (e->h_leaf) (void)hipHostFree(e->h_leaf);
+    if (e->h_eval) (void)hipHostFree(e->h_eval);
     if (e->h_move) (void)hipHostFree(e->h_move);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -2249,7 +2287,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
                      dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
         if ((rc = check_launch())) return rc;
         timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
-                     (int32_t *)nullptr, (int32_t)0);
+                     (int32_t *)nullptr, (int32_t)0, (HostLeaf *)nullptr);
         if ((rc = check_launch())) return rc;
         HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2297,7 +2335,8 @@ static int select_async_impl(uttt_engine_t *e, int32_t *host_count, int32_t tag)
     timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)),
                  dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
     if ((rc = check_launch())) return rc;
-    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count, tag);
+    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count, tag,
+                 (HostLeaf *)nullptr);
     if ((rc = check_launch())) return rc;
     e->n_pending = -1;
     e->phase = 3;
@@ -2337,6 +2376,87 @@ int uttt_search_pending(uttt_engine_t *e, uttt_state_t *states, int32_t *copies)
         if (states) states[i] = leaf[tree_of[i]];
         if (copies) copies[i] = rec[tree_of[i]].k;
     }
+    return UTTT_OK;
+}
+
+// Wait for a tag the device stores into fine-grained host memory (k_scan): spin, no stream sync.
+static int wait_host_tag(uttt_engine *e, const int32_t *tag_word, int32_t tag) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(tag_word, __ATOMIC_ACQUIRE) == tag) return UTTT_OK;
+        if ((it & 1023u) == 0u) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                set_error("engine stream failed: %s", hipGetErrorString(q));
+                return UTTT_ERR_HIP;
+            }
+            if (q == hipSuccess && __atomic_load_n(tag_word, __ATOMIC_ACQUIRE) != tag) {
+                set_error("engine: the stream drained without storing the round's tag");
+                return UTTT_ERR_HIP;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                set_error("engine: round result not stored within 60 s");
+                return UTTT_ERR_HIP;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+int uttt_search_select_host(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending) {
+    if (!e || !leaf || !copies || !n_pending) return UTTT_ERR_ARG;
+    if (e->tr.n_trees != 1) {
+        set_error("uttt_search_select_host: one-tree searches only (uttt_search_begin with n_trees = 1)");
+        return UTTT_ERR_ARG;
+    }
+    if (e->phase != 1) {
+        set_error("uttt_search_select_host: call uttt_search_begin (or apply the previous round) first");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = 0, n = 0;
+    for (;;) {  // the select budget may stop the tree before it queues a leaf: select again (as uttt_search_select)
+        timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(1)), dim3(kBlock),
+                     e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
+        if ((rc = check_launch())) return rc;
+        const int32_t tag = ++e->leaf_tag;
+        timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
+                     (int32_t *)nullptr, tag, e->h_leaf);
+        if ((rc = check_launch())) return rc;
+        if ((rc = wait_host_tag(e, &e->h_leaf->tag, tag))) return rc;
+        n = __atomic_load_n(&e->h_leaf->count, __ATOMIC_ACQUIRE);
+        if (e->timing) drain_events(e);
+        if (n > 0 || __atomic_load_n(&e->h_leaf->stopped, __ATOMIC_ACQUIRE) == 0) break;
+    }
+    if (n > 0) {
+        memcpy(leaf, const_cast<const uttt_state_t *>(&e->h_leaf->state), sizeof(uttt_state_t));
+        *copies = e->h_leaf->k;
+    }
+    *n_pending = n;
+    e->n_pending = n;
+    e->phase = n > 0 ? 2 : 1;
+    return UTTT_OK;
+}
+
+int uttt_search_apply_host(uttt_engine_t *e, const float *policy, float value) {
+    if (!e || !policy) return UTTT_ERR_ARG;
+    if (e->phase != 2 || e->n_pending != 1 || e->tr.n_trees != 1) {
+        set_error("uttt_search_apply_host: no pending leaf of a one-tree search (call uttt_search_select_host)");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    // the previous k_apply that read h_eval completed before this round's k_scan stored its tag, which the
+    // host has seen (stream order): the buffer is free to rewrite
+    memcpy(e->h_eval, policy, 81 * sizeof(float));
+    e->h_eval[81] = value;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    timed_launch(e, kKApply, k_apply, dim3(grid_waves(1)), dim3(kBlock), e->pool, e->tr, e->cache,
+                 (const float *)e->h_eval, (int64_t)96, (const float *)(e->h_eval + 81), (int64_t)1,
+                 (const int32_t *)nullptr, 0, bytes_ptr(e, kKApply));
+    int rc = check_launch();
+    if (rc) return rc;
+    e->phase = 1;
+    e->n_pending = 0;
     return UTTT_OK;
 }
 

@@ -127,6 +127,34 @@ py::list pv_mcts_scores(py::object model, const State &state, float temperature,
     uttt_engine_t *eng = search_engine().get(evaluate_count);
     check(uttt_search_begin(eng, &state.s, 1, evaluate_count, batch_size));
     std::vector<float> pol, val;
+    if (dedup) {
+        // one state per flush: the round's leaf comes back through pinned host memory the scan writes, the
+        // result goes to pinned memory k_apply reads (uttt_search_select_host / _apply_host): no copy
+        // operation and no stream synchronisation per flush besides the model's own
+        float p81[81];
+        for (;;) {
+            int32_t n = 0, k = 0;
+            uttt_state_t leaf;
+            check(uttt_search_select_host(eng, &leaf, &k, &n));
+            if (n == 0) break;
+            py::list batch;
+            batch.append(py::cast(State(leaf)));
+            py::object result = model(batch);
+            float v = 0.0f;
+            bool got = false;
+            for (auto item : result) {
+                read_result(item, p81, &v);
+                got = true;
+                break;
+            }
+            if (!got) throw std::runtime_error("model returned 0 results for 1 states");
+            check(uttt_search_apply_host(eng, p81, v));
+        }
+        float scores[81];
+        int32_t L = 0;
+        check(uttt_search_scores(eng, temperature, scores, &L));
+        return py::cast(std::vector<float>(scores, scores + L));
+    }
     for (;;) {
         int32_t n = 0;
         check(uttt_search_select(eng, nullptr, &n));
