@@ -43,6 +43,56 @@ def main():
         torch.cuda.synchronize()
         out[name] = round((time.perf_counter() - t) * 1e3 / len(states), 3)
     os.environ.pop("UTTT_EVALUATOR")
+    # the same searches on the reference's own uttt_cpp (oracle/_ref, compiled from its sources; present where
+    # the build ran __graft_entry__.build() beside /root/reference) with the reference's own flush glue
+    # (pv_mcts_cpp.py:37-87: k states per flush, to_input_tensor each, NCHW torch tensor, model, .cpu()), and
+    # this build's uttt_cpp under the same glue: the per-search difference is the module's own cost
+    ref_dir = os.path.join(REPO, "oracle", "_ref")
+    glue_calls = {"n": 0, "states": 0, "s": 0.0}
+
+    def ref_glue(states_list):
+        t0 = time.perf_counter()
+        x = np.asarray([s.to_input_tensor() for s in states_list], dtype=np.float32).reshape(-1, 9, 9, 3)
+        x = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 3, 1, 2))).to("cuda")
+        with torch.no_grad():
+            p, v = net(x)
+        p, v = p.cpu().numpy(), v.cpu().numpy()
+        res = [(p[i], float(v[i][0])) for i in range(len(states_list))]
+        glue_calls["n"] += 1
+        glue_calls["states"] += len(states_list)
+        glue_calls["s"] += time.perf_counter() - t0
+        return res
+
+    mods = [("this_uttt_cpp_reference_glue", uttt_cpp, {"dedup": False}),
+            ("this_uttt_cpp_reference_glue_dedup", uttt_cpp, {})]
+    if os.path.isdir(ref_dir):
+        import importlib.machinery
+        import importlib.util
+        path = [os.path.join(ref_dir, f) for f in os.listdir(ref_dir) if f.startswith("uttt_cpp")][0]
+        # the reference module's init function is PyInit_uttt_cpp: load it under that name, outside sys.modules
+        loader = importlib.machinery.ExtensionFileLoader("uttt_cpp", path)
+        spec = importlib.util.spec_from_file_location("uttt_cpp", path, loader=loader)
+        ref_mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(ref_mod)
+        mods.insert(0, ("reference_uttt_cpp_reference_glue", ref_mod, {}))
+    out["same_glue"] = {}
+    for name, mod, kw in mods:
+        sts = [mod.State(s.pieces, s.enemy_pieces, s.main_board_pieces, s.main_board_enemy_pieces, s.active_board)
+               for s in states]
+        for st in sts[:3]:
+            mod.pv_mcts_scores(model=ref_glue, state=st, temperature=1.0, evaluate_count=50, batch_size=8, **kw)
+        torch.cuda.synchronize()
+        glue_calls.update(n=0, states=0, s=0.0)
+        t = time.perf_counter()
+        for st in sts:
+            mod.pv_mcts_scores(model=ref_glue, state=st, temperature=1.0, evaluate_count=50, batch_size=8, **kw)
+        torch.cuda.synchronize()
+        tot = (time.perf_counter() - t) * 1e3 / len(sts)
+        out["same_glue"][name] = {"ms_per_search": round(tot, 3), "sims_per_s": round(50e3 / tot, 1),
+                                  "flushes_per_search": round(glue_calls["n"] / len(sts), 2),
+                                  "states_per_flush": round(glue_calls["states"] / max(glue_calls["n"], 1), 2),
+                                  "glue_ms_per_search": round(glue_calls["s"] * 1e3 / len(sts), 3),
+                                  "module_ms_per_search": round(tot - glue_calls["s"] * 1e3 / len(sts), 3)}
     out["positions"] = len(states)
     # self_play_cpp.self_play's 500 games one move at a time: 26,651 plies in the build's 500-game cycle
     # (profiles/r3/cycle_fp32_final.json), i.e. 53.3 moves per game
