@@ -165,10 +165,12 @@ int uttt_search_pending(uttt_engine_t *eng, uttt_state_t *states, int32_t *copie
  * without a copy operation or a stream synchronisation per flush (round 5): select_host launches the
  * select and the scan, which stores the counts, the pending leaf's state and its copies k into fine-grained
  * pinned host memory and then a tag the host spins on; apply_host copies the leaf's evaluation (81 priors
- * by action, value) into pinned host memory that k_apply reads directly, and returns without waiting.
- * Same results as uttt_search_select + uttt_search_pending + uttt_search_apply (one result per leaf). */
+ * by action, value; one row or one per copy) into pinned host memory that k_apply reads directly, and
+ * returns without waiting. Same results as uttt_search_select + uttt_search_pending + uttt_search_apply. */
 int uttt_search_select_host(uttt_engine_t *eng, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending);
-int uttt_search_apply_host(uttt_engine_t *eng, const float *policy81, float value);
+int uttt_search_apply_host(uttt_engine_t *eng, const float *policy, int64_t policy_stride, const float *value,
+                           int32_t rows);  /* rows: 1 (one result for the leaf's k copies) or k (one per copy,
+                                              applied in order: the reference's call pattern) */
 
 /* Evaluator results for the pending leaves (uttt_mcts.cpp:138-167: legal-mask,
  * sequential f32 renormalisation, expand k times, back up k times).

@@ -271,6 +271,16 @@ def test_uttt_cpp_callback_search_matches_golden(gpu):
             assert len(calls) == d["flushes"][r]
             if not dedup:
                 assert sum(calls) == d["evals"][r]
+    # the default is the reference's call pattern (python_bindings.cpp:11-47): the k queued copies per flush
+    r = rows[0]
+    i = int(d["pos"][r])
+    st = uttt_cpp.State(d["pos_pieces"][i].reshape(9, 9).tolist(), d["pos_enemy"][i].reshape(9, 9).tolist(),
+                        d["pos_main_p"][i].tolist(), d["pos_main_e"][i].tolist(), int(d["pos_active"][i]))
+    calls.clear()
+    sc = np.asarray(uttt_cpp.pv_mcts_scores(model=model, state=st, temperature=float(d["temp"][r]),
+                                            evaluate_count=int(d["sims"][r]), batch_size=int(d["batch"][r])), np.float32)
+    assert np.array_equal(sc.view(np.uint32), d["scores"][r][:int(d["n"][r])].view(np.uint32))
+    assert len(calls) == d["flushes"][r] and sum(calls) == d["evals"][r]
 
 
 def test_network_gpu_matches_cpu_fp32(gpu):

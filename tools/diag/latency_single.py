@@ -93,6 +93,20 @@ def main():
                                   "states_per_flush": round(glue_calls["states"] / max(glue_calls["n"], 1), 2),
                                   "glue_ms_per_search": round(glue_calls["s"] * 1e3 / len(sts), 3),
                                   "module_ms_per_search": round(tot - glue_calls["s"] * 1e3 / len(sts), 3)}
+    # the modules alone: a model that returns fixed arrays (no device work), so a search's time is the module's
+    # own (the reference's CPU tree; this build's select / apply kernels and the per-flush host round trip)
+    fixed_p, fixed_v = np.full(81, 1.0 / 81, np.float32), 0.0
+    out["module_only"] = {}
+    for name, mod, kw in mods:
+        sts = [mod.State(s.pieces, s.enemy_pieces, s.main_board_pieces, s.main_board_enemy_pieces, s.active_board)
+               for s in states]
+        fixed = lambda sl: [(fixed_p, fixed_v)] * len(sl)  # noqa: E731
+        for st in sts[:3]:
+            mod.pv_mcts_scores(model=fixed, state=st, temperature=1.0, evaluate_count=50, batch_size=8, **kw)
+        t = time.perf_counter()
+        for st in sts:
+            mod.pv_mcts_scores(model=fixed, state=st, temperature=1.0, evaluate_count=50, batch_size=8, **kw)
+        out["module_only"][name] = round((time.perf_counter() - t) * 1e3 / len(sts), 4)
     out["positions"] = len(states)
     # self_play_cpp.self_play's 500 games one move at a time: 26,651 plies in the build's 500-game cycle
     # (profiles/r3/cycle_fp32_final.json), i.e. 53.3 moves per game

@@ -1915,7 +1915,9 @@ struct uttt_engine {
     int32_t *h_count = nullptr;  // pinned
     int32_t *h_ring = nullptr;   // fine-grained pinned: kCountRing x {pending, stopped, left, tag}, k_scan-written
     HostLeaf *h_leaf = nullptr;  // fine-grained pinned: a one-tree round's result (uttt_search_select_host)
-    float *h_eval = nullptr;     // fine-grained pinned: its evaluation, read by k_apply (uttt_search_apply_host)
+    float *h_eval = nullptr;     // fine-grained pinned: its evaluation, read by k_apply (uttt_search_apply_host):
+                                 // [rows][96] policy, [rows] value, one int32 0 (the per-copy row base)
+    int64_t h_eval_rows = 0;
     int32_t leaf_tag = 0;
     int32_t *d_rowbase = nullptr;
     float *d_pol_scratch = nullptr;
@@ -2161,13 +2163,11 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         return fail(UTTT_ERR_HIP);
     }
     memset(e->h_ring, 0, sizeof(int32_t) * 4 * kCountRing);
-    if (hipHostMalloc((void **)&e->h_leaf, sizeof(HostLeaf), hipHostMallocCoherent) != hipSuccess ||
-        hipHostMalloc((void **)&e->h_eval, sizeof(float) * 96, hipHostMallocCoherent) != hipSuccess) {
+    if (hipHostMalloc((void **)&e->h_leaf, sizeof(HostLeaf), hipHostMallocCoherent) != hipSuccess) {
         set_error("hipHostMalloc failed");
         return fail(UTTT_ERR_HIP);
     }
     memset(e->h_leaf, 0, sizeof(HostLeaf));
-    memset(e->h_eval, 0, sizeof(float) * 96);
     if (hipHostMalloc((void **)&e->h_count, sizeof(int32_t) * 4, hipHostMallocDefault) != hipSuccess) {
         set_error("hipHostMalloc failed");
         return fail(UTTT_ERR_HIP);
@@ -2438,21 +2438,48 @@ int uttt_search_select_host(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copie
     return UTTT_OK;
 }
 
-int uttt_search_apply_host(uttt_engine_t *e, const float *policy, float value) {
-    if (!e || !policy) return UTTT_ERR_ARG;
+int uttt_search_apply_host(uttt_engine_t *e, const float *policy, int64_t pld, const float *value, int32_t rows) {
+    if (!e || !policy || !value || pld < 81 || rows < 1) {
+        set_error("uttt_search_apply_host: bad arguments (policy stride must be >= 81, rows >= 1)");
+        return UTTT_ERR_ARG;
+    }
     if (e->phase != 2 || e->n_pending != 1 || e->tr.n_trees != 1) {
         set_error("uttt_search_apply_host: no pending leaf of a one-tree search (call uttt_search_select_host)");
         return UTTT_ERR_ORDER;
     }
+    const int32_t k = e->h_leaf->k;
+    if (rows != 1 && rows != k) {
+        set_error("uttt_search_apply_host: %d results for a leaf queued %d times (pass 1 or %d)", rows, k, k);
+        return UTTT_ERR_ARG;
+    }
     HIP_TRY(hipSetDevice(e->device));
-    // the previous k_apply that read h_eval completed before this round's k_scan stored its tag, which the
-    // host has seen (stream order): the buffer is free to rewrite
-    memcpy(e->h_eval, policy, 81 * sizeof(float));
-    e->h_eval[81] = value;
+    if (rows > e->h_eval_rows) {
+        // grown between rounds only: the k_apply that last read the buffer completed before this round's
+        // scan stored its tag (stream order), which the host has seen
+        if (e->h_eval) (void)hipHostFree(e->h_eval);
+        e->h_eval = nullptr;
+        int64_t cap = e->h_eval_rows ? e->h_eval_rows : 16;
+        while (cap < rows) cap *= 2;
+        if (hipHostMalloc((void **)&e->h_eval, (size_t)cap * 97 * sizeof(float) + 16, hipHostMallocCoherent) != hipSuccess) {
+            e->h_eval_rows = 0;
+            set_error("hipHostMalloc failed");
+            return UTTT_ERR_HIP;
+        }
+        e->h_eval_rows = cap;
+        reinterpret_cast<int32_t *>(e->h_eval + cap * 97)[0] = 0;  // the per-copy row base of slot 0
+    }
+    float *hp = e->h_eval, *hv = e->h_eval + e->h_eval_rows * 96;
+    for (int32_t r = 0; r < rows; ++r) {
+        memcpy(hp + (size_t)r * 96, policy + (size_t)r * pld, 81 * sizeof(float));
+        hv[r] = value[r];
+    }
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    timed_launch(e, kKApply, k_apply, dim3(grid_waves(1)), dim3(kBlock), e->pool, e->tr, e->cache,
-                 (const float *)e->h_eval, (int64_t)96, (const float *)(e->h_eval + 81), (int64_t)1,
-                 (const int32_t *)nullptr, 0, bytes_ptr(e, kKApply));
+    const int per_copy = rows > 1 ? 1 : 0;  // k copies applied in order (the reference's call pattern)
+    EvalCache c = per_copy ? EvalCache{} : e->cache;
+    timed_launch(e, kKApply, k_apply, dim3(grid_waves(1)), dim3(kBlock), e->pool, e->tr, c, (const float *)hp,
+                 (int64_t)96, (const float *)hv, (int64_t)1,
+                 (const int32_t *)reinterpret_cast<int32_t *>(e->h_eval + e->h_eval_rows * 97), per_copy,
+                 bytes_ptr(e, kKApply));
     int rc = check_launch();
     if (rc) return rc;
     e->phase = 1;

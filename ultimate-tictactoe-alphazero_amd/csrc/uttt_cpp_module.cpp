@@ -126,42 +126,15 @@ py::list pv_mcts_scores(py::object model, const State &state, float temperature,
     }
     uttt_engine_t *eng = search_engine().get(evaluate_count);
     check(uttt_search_begin(eng, &state.s, 1, evaluate_count, batch_size));
+    // per flush: the round's leaf and its copies k come back through pinned host memory the scan writes
+    // (uttt_search_select_host), the results go to pinned memory k_apply reads (uttt_search_apply_host): no
+    // copy operation and no stream synchronisation per flush besides the model's own
     std::vector<float> pol, val;
-    if (dedup) {
-        // one state per flush: the round's leaf comes back through pinned host memory the scan writes, the
-        // result goes to pinned memory k_apply reads (uttt_search_select_host / _apply_host): no copy
-        // operation and no stream synchronisation per flush besides the model's own
-        float p81[81];
-        for (;;) {
-            int32_t n = 0, k = 0;
-            uttt_state_t leaf;
-            check(uttt_search_select_host(eng, &leaf, &k, &n));
-            if (n == 0) break;
-            py::list batch;
-            batch.append(py::cast(State(leaf)));
-            py::object result = model(batch);
-            float v = 0.0f;
-            bool got = false;
-            for (auto item : result) {
-                read_result(item, p81, &v);
-                got = true;
-                break;
-            }
-            if (!got) throw std::runtime_error("model returned 0 results for 1 states");
-            check(uttt_search_apply_host(eng, p81, v));
-        }
-        float scores[81];
-        int32_t L = 0;
-        check(uttt_search_scores(eng, temperature, scores, &L));
-        return py::cast(std::vector<float>(scores, scores + L));
-    }
     for (;;) {
-        int32_t n = 0;
-        check(uttt_search_select(eng, nullptr, &n));
-        if (n == 0) break;
+        int32_t n = 0, k = 0;
         uttt_state_t leaf;
-        int32_t k = 0;
-        check(uttt_search_pending(eng, &leaf, &k));
+        check(uttt_search_select_host(eng, &leaf, &k, &n));
+        if (n == 0) break;
         const int copies = dedup ? 1 : k;
         py::list batch;
         for (int i = 0; i < copies; ++i) batch.append(py::cast(State(leaf)));
@@ -177,7 +150,7 @@ py::list pv_mcts_scores(py::object model, const State &state, float temperature,
         if (got < copies)
             throw std::runtime_error("model returned " + std::to_string(got) + " results for " + std::to_string(copies) +
                                      " states");
-        check(uttt_search_apply(eng, pol.data(), 81, val.data(), 1, dedup ? 0 : 1, 0));
+        check(uttt_search_apply_host(eng, pol.data(), 81, val.data(), copies));
     }
     float scores[81];
     int32_t L = 0;
@@ -290,8 +263,10 @@ PYBIND11_MODULE(_uttt_cpp, m) {
         .def_readwrite("value", &InferenceResult::value);
 
     m.def("pv_mcts_scores", &pv_mcts_scores, py::arg("model"), py::arg("state"), py::arg("temperature") = 0.0f,
-          py::arg("evaluate_count") = 50, py::arg("batch_size") = 8, py::arg("dedup") = true,
-          "Run MCTS (on the MI355X engine) and return score distribution over legal actions");
+          py::arg("evaluate_count") = 50, py::arg("batch_size") = 8, py::arg("dedup") = false,
+          "Run MCTS (on the MI355X engine) and return score distribution over legal actions. The model gets the k "
+          "identical queued states of each flush, as the reference's module passes them (python_bindings.cpp:11-47); "
+          "dedup=True hands it one state and applies its result k times (same scores for a deterministic model)");
     m.def(
         "boltzman",
         [](const std::vector<float> &xs, float temperature) {

@@ -55,6 +55,7 @@ def make_inference_func(model, evaluator=None):
             p, v = p.cpu().numpy(), v.cpu().numpy()
             return [(p[i], float(v[i])) for i in range(n)]
 
+        fused_inference.fused = True
         return fused_inference
     dev = _model_device(model)
 
@@ -74,8 +75,13 @@ def pv_mcts_scores_cpp(model, state, temperature, evaluate_count=50, batch_size=
     if not CPP_AVAILABLE:
         raise RuntimeError("C++ module is not available. Please build uttt_cpp first.")
     model.eval()
-    scores = uttt_cpp.pv_mcts_scores(model=make_inference_func(model), state=_to_engine_state(state),
-                                     temperature=temperature, evaluate_count=evaluate_count, batch_size=batch_size)
+    fn = make_inference_func(model)
+    # the fused HIP evaluator takes the flush's one distinct state (the k queued copies are identical, no
+    # virtual loss); the PyTorch forward gets the reference's k copies (MIOpen's batch-1 convolutions ran
+    # slower than its batch-k ones: 13.2 against 11.0 ms of model time per search, profiles/r5/latency_single.json)
+    scores = uttt_cpp.pv_mcts_scores(model=fn, state=_to_engine_state(state), temperature=temperature,
+                                     evaluate_count=evaluate_count, batch_size=batch_size,
+                                     dedup=getattr(fn, "fused", False))
     return np.array(scores)
 
 
