@@ -815,13 +815,14 @@ __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int firs
     clk.mark<kSpPuct>();
 }
 
+// The descent of one tree by one wave (k_select's body; k_flush1 runs it after the previous flush's apply).
+// cv_row: this wave's 84-float LDS row (a cache hit's values). host_leaf (one-tree searches only): the
+// round's counts, the queued leaf and its copies go to fine-grained host memory behind `tag`, and the
+// round's device counts / slot 0 are written here (there is no k_scan launch in that form).
 template <bool PY>
-__global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalCache cache,
-                                                   unsigned long long *stats) {
-    __shared__ __attribute__((aligned(16))) float s_hit[kWavesPerBlock][84];  // a cache hit's values, per wave
+__device__ __forceinline__ void select_wave(Pool pool, Trees tr, EvalCache cache, unsigned long long *stats, int t,
+                                            float *cv_row, HostLeaf *host_leaf, int32_t tag) {
     const int lane = lane_id();
-    const int t = wave_index();
-    if (t >= tr.n_trees) return;
     TreeCtl ctl = tr.ctl[t];
     int pend = 0;
     unsigned long long bytes = 0;
@@ -1001,7 +1002,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             // Unexpanded leaf (n == 0 && no children, uttt_mcts.cpp:121): queue it with
             // k = the copies the reference would queue before flushing (:127).
             const int k = min(tr.batch, tr.sims - sims_done);
-            float *cv = s_hit[threadIdx.x >> 6];
+            float *cv = cv_row;
             trips += cache.flag ? 1 : 0;
             const bool hit = cache_lookup(cache, s, cv);
             clk.mark<kSpProbe>();
@@ -1073,7 +1074,36 @@ __global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalC
             atomicAdd(stripe_of(stats + kKSelTrips * kRow), (unsigned long long)trips);
             atomicMax(stripe_of(stats + kKSelTripMax * kRow), (unsigned long long)trips);
         }
+        if (host_leaf) {  // one tree: what k_scan would derive from pending[0]
+            const int p = pend & 0xFF, c0 = (p == 1 || p == 3) ? 1 : 0, c1 = p == 2 ? 1 : 0, c2 = p >= 2 ? 1 : 0;
+            tr.count[0] = c0;
+            tr.count[1] = c1;
+            tr.count[2] = c2;
+            tr.tree_of[0] = t;
+            tr.depth_of[0] = pend >> 8;
+            __hip_atomic_store(&host_leaf->count, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_leaf->stopped, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host_leaf->left, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (c0) {
+                const uttt_state_t st = tr.leaf[t];  // stored by this lane above
+                const int32_t *w = reinterpret_cast<const int32_t *>(&st);
+                int32_t *d = reinterpret_cast<int32_t *>(&host_leaf->state);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&host_leaf->k, tr.rec[t].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __hip_atomic_store(&host_leaf->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
+}
+
+template <bool PY>
+__global__ __launch_bounds__(kBlock, 4) void k_select(Pool pool, Trees tr, EvalCache cache,
+                                                   unsigned long long *stats) {
+    __shared__ __attribute__((aligned(16))) float s_hit[kWavesPerBlock][84];  // a cache hit's values, per wave
+    const int t = wave_index();
+    if (t >= tr.n_trees) return;
+    select_wave<PY>(pool, tr, cache, stats, t, s_hit[threadIdx.x >> 6], nullptr, 0);
 }
 
 // ------------------------------------------------------------------- scan --
@@ -1111,8 +1141,7 @@ __device__ __forceinline__ T block_scan_1024(T v, T *total, T *wsum /* __shared_
 // without a copy operation on the stream (round 4: one stream operation less per round). Round 5: word 3
 // gets the round's tag after them (a system-scope release store), so a host that polls the tag needs no
 // event either (uttt_round_hash_async).
-__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count, int32_t tag,
-                                               HostLeaf *host_leaf) {
+__global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *stats, int32_t *host_count, int32_t tag) {
     __shared__ unsigned long long wsum[16];
     const int tid = threadIdx.x;
     if (stats && tid < 64) {  // the select launch before this scan is complete: fold its slowest tree
@@ -1169,20 +1198,6 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
             __hip_atomic_store(host_count + 2, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 3, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        if (host_leaf) {  // a one-tree engine: tree 0 is slot 0's
-            __hip_atomic_store(&host_leaf->count, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&host_leaf->stopped, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&host_leaf->left, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (c0 > 0) {
-                const uttt_state_t st = tr.leaf[0];
-                const int32_t *w = reinterpret_cast<const int32_t *>(&st);
-                int32_t *d = reinterpret_cast<int32_t *>(&host_leaf->state);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&host_leaf->k, tr.rec[0].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            __hip_atomic_store(&host_leaf->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
     }
 }
 
@@ -1212,13 +1227,11 @@ __global__ __launch_bounds__(256) void k_encode(Trees tr, float *__restrict__ x,
 // legal priors, sequential f32 sum in action order, divide (uniform 1/|legal|
 // if sum <= 0), append the child block, back up the value along the path.
 // per_copy: row rowbase[slot] + j holds copy j's result; else row = slot.
-__global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache cache, const float *__restrict__ policy,
-                                                  int64_t pld, const float *__restrict__ value, int64_t vld,
-                                                  const int32_t *__restrict__ rowbase, int per_copy,
-                                                  unsigned long long *bytes_ctr) {
-    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];  // the prior sum's row, per wave
+__device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache, const float *__restrict__ policy,
+                                           int64_t pld, const float *__restrict__ value, int64_t vld,
+                                           const int32_t *__restrict__ rowbase, int per_copy,
+                                           unsigned long long *bytes_ctr, int slot, float *row /* LDS, 84 floats */) {
     const int lane = lane_id();
-    const int slot = wave_index();
     // two dependent round trips before the work: the count with this slot's tree and leaf depth
     // (tree_of / depth_of hold n_trees entries, stale past the count), then the tree's records, the
     // path entries 0..depth (round 4: all 128 were loaded, 2.5 KB a leaf) and the slot's evaluation
@@ -1280,7 +1293,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
         const bool cacheable = __ballot(!fin0 || (lane < 17 && !fin1)) == 0ull;
         float psum = 0.0f;
         if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, pr_lo, pr_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f,
-                           v, ctl.node_count, tr.py != 0, s_row[threadIdx.x >> 6], false, 0.0f, &psum)) {
+                           v, ctl.node_count, tr.py != 0, row, false, 0.0f, &psum)) {
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
@@ -1370,6 +1383,34 @@ __global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache
             atomicAdd(stripe_of(bytes_ctr), b);
         }
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_apply(Pool pool, Trees tr, EvalCache cache, const float *__restrict__ policy,
+                                                  int64_t pld, const float *__restrict__ value, int64_t vld,
+                                                  const int32_t *__restrict__ rowbase, int per_copy,
+                                                  unsigned long long *bytes_ctr) {
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];  // the prior sum's row, per wave
+    apply_wave(pool, tr, cache, policy, pld, value, vld, rowbase, per_copy, bytes_ctr, wave_index(),
+               s_row[threadIdx.x >> 6]);
+}
+
+// One flush of a one-tree search in one launch (round 5, uttt_search_select_host / _apply_host): the previous
+// flush's evaluation applied (k_apply's body, reading it from pinned host memory), then the next descent
+// (k_select's body), which stores the round's result to pinned host memory behind its tag. One wave, one
+// dispatch per flush where k_apply, k_select and k_scan took three.
+template <bool PY>
+__global__ __launch_bounds__(kWave) void k_flush1(Pool pool, Trees tr, EvalCache cache, EvalCache apply_cache,
+                                                  const float *__restrict__ policy, int64_t pld,
+                                                  const float *__restrict__ value, int64_t vld,
+                                                  const int32_t *__restrict__ rowbase, int per_copy, int do_apply,
+                                                  unsigned long long *stats, HostLeaf *host_leaf, int32_t tag) {
+    __shared__ __attribute__((aligned(16))) float s_row[84];
+    if (do_apply) {
+        apply_wave(pool, tr, apply_cache, policy, pld, value, vld, rowbase, per_copy,
+                   stats ? stats + kKApply * kRow : nullptr, 0, s_row);
+        wave_memory_fence();  // the descent reads the records the apply wrote
+    }
+    select_wave<PY>(pool, tr, cache, stats, 0, s_row, host_leaf, tag);
 }
 
 // -------------------------------------------------------------- hash eval --
@@ -1918,6 +1959,8 @@ struct uttt_engine {
     float *h_eval = nullptr;     // fine-grained pinned: its evaluation, read by k_apply (uttt_search_apply_host):
                                  // [rows][96] policy, [rows] value, one int32 0 (the per-copy row base)
     int64_t h_eval_rows = 0;
+    int32_t host_apply_rows = 0;  // a one-tree evaluation staged by uttt_search_apply_host, applied by the next
+                                  // k_flush1 (or by flush_host_apply before any other call that reads the tree)
     int32_t leaf_tag = 0;
     int32_t *d_rowbase = nullptr;
     float *d_pol_scratch = nullptr;
@@ -2260,6 +2303,7 @@ int uttt_search_begin_mode(uttt_engine_t *e, const uttt_state_t *roots, int32_t 
         return UTTT_ERR_ARG;
     }
     HIP_TRY(hipSetDevice(e->device));
+    e->host_apply_rows = 0;  // a staged evaluation of the previous search is dropped with it
     int rc = search_begin_common(e, n_trees, sims, batch);
     if (rc) return rc;
     e->tr.py = semantics == UTTT_SEMANTICS_PY ? 1 : 0;
@@ -2271,6 +2315,8 @@ int uttt_search_begin_mode(uttt_engine_t *e, const uttt_state_t *roots, int32_t 
     return check_launch();
 }
 
+static int flush_host_apply(uttt_engine *e);
+
 int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
     if (!e || !n_pending) return UTTT_ERR_ARG;
     if (e->phase != 1) {
@@ -2278,6 +2324,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
         return UTTT_ERR_ORDER;
     }
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = flush_host_apply(e)) return rc0;
     int rc = 0, n = 0;
     // trees stopped by the select budget resume in the next launch; when no tree has a
     // leaf but some were stopped, select again (every launch completes >= 1 simulation
@@ -2287,7 +2334,7 @@ int uttt_search_select(uttt_engine_t *e, float *nn_input, int32_t *n_pending) {
                      dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
         if ((rc = check_launch())) return rc;
         timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
-                     (int32_t *)nullptr, (int32_t)0, (HostLeaf *)nullptr);
+                     (int32_t *)nullptr, (int32_t)0);
         if ((rc = check_launch())) return rc;
         HIP_TRY(hipMemcpyAsync(e->h_count, e->tr.count, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2331,12 +2378,12 @@ static int select_async_impl(uttt_engine_t *e, int32_t *host_count, int32_t tag)
         return UTTT_ERR_ORDER;
     }
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = flush_host_apply(e)) return rc0;
     int rc = 0;
     timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(e->tr.n_trees)),
                  dim3(kBlock), e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
     if ((rc = check_launch())) return rc;
-    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count, tag,
-                 (HostLeaf *)nullptr);
+    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr, host_count, tag);
     if ((rc = check_launch())) return rc;
     e->n_pending = -1;
     e->phase = 3;
@@ -2403,6 +2450,35 @@ static int wait_host_tag(uttt_engine *e, const int32_t *tag_word, int32_t tag) {
     }
 }
 
+// The staged evaluation's k_apply arguments (pinned host memory; rows 1: one row for the leaf's k copies,
+// rows k: one per copy, applied in order, the evaluation cache bypassed as in uttt_search_apply).
+struct HostApplyArgs {
+    const float *policy, *value;
+    const int32_t *rowbase;
+    int per_copy;
+    EvalCache cache;
+};
+static HostApplyArgs host_apply_args(uttt_engine *e) {
+    HostApplyArgs a;
+    a.policy = e->h_eval;
+    a.value = e->h_eval + e->h_eval_rows * 96;
+    a.rowbase = reinterpret_cast<const int32_t *>(e->h_eval + e->h_eval_rows * 97);
+    a.per_copy = e->host_apply_rows > 1 ? 1 : 0;
+    a.cache = a.per_copy ? EvalCache{} : e->cache;
+    return a;
+}
+
+// A staged one-tree evaluation that no k_flush1 has applied yet, applied now (any call other than
+// uttt_search_select_host that reads or restarts the tree)
+static int flush_host_apply(uttt_engine *e) {
+    if (!e->host_apply_rows) return UTTT_OK;
+    const HostApplyArgs a = host_apply_args(e);
+    e->host_apply_rows = 0;
+    timed_launch(e, kKApply, k_apply, dim3(grid_waves(1)), dim3(kBlock), e->pool, e->tr, a.cache, a.policy,
+                 (int64_t)96, a.value, (int64_t)1, a.rowbase, a.per_copy, bytes_ptr(e, kKApply));
+    return check_launch();
+}
+
 int uttt_search_select_host(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending) {
     if (!e || !leaf || !copies || !n_pending) return UTTT_ERR_ARG;
     if (e->tr.n_trees != 1) {
@@ -2416,12 +2492,14 @@ int uttt_search_select_host(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copie
     HIP_TRY(hipSetDevice(e->device));
     int rc = 0, n = 0;
     for (;;) {  // the select budget may stop the tree before it queues a leaf: select again (as uttt_search_select)
-        timed_launch(e, kKSelect, e->tr.py ? k_select<true> : k_select<false>, dim3(grid_waves(1)), dim3(kBlock),
-                     e->pool, e->tr, e->cache, e->timing ? e->d_bytes : nullptr);
-        if ((rc = check_launch())) return rc;
         const int32_t tag = ++e->leaf_tag;
-        timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
-                     (int32_t *)nullptr, tag, e->h_leaf);
+        const int do_apply = e->host_apply_rows ? 1 : 0;
+        HostApplyArgs a = host_apply_args(e);
+        e->host_apply_rows = 0;
+        e->launches[kKApply] += do_apply;
+        timed_launch(e, kKSelect, e->tr.py ? k_flush1<true> : k_flush1<false>, dim3(1), dim3(kWave), e->pool, e->tr,
+                     e->cache, a.cache, a.policy, (int64_t)96, a.value, (int64_t)1, a.rowbase, a.per_copy, do_apply,
+                     e->timing ? e->d_bytes : nullptr, e->h_leaf, tag);
         if ((rc = check_launch())) return rc;
         if ((rc = wait_host_tag(e, &e->h_leaf->tag, tag))) return rc;
         n = __atomic_load_n(&e->h_leaf->count, __ATOMIC_ACQUIRE);
@@ -2454,8 +2532,8 @@ int uttt_search_apply_host(uttt_engine_t *e, const float *policy, int64_t pld, c
     }
     HIP_TRY(hipSetDevice(e->device));
     if (rows > e->h_eval_rows) {
-        // grown between rounds only: the k_apply that last read the buffer completed before this round's
-        // scan stored its tag (stream order), which the host has seen
+        // grown between rounds only: the k_flush1 that last read the buffer completed before it stored the
+        // tag the host has seen
         if (e->h_eval) (void)hipHostFree(e->h_eval);
         e->h_eval = nullptr;
         int64_t cap = e->h_eval_rows ? e->h_eval_rows : 16;
@@ -2473,15 +2551,8 @@ int uttt_search_apply_host(uttt_engine_t *e, const float *policy, int64_t pld, c
         memcpy(hp + (size_t)r * 96, policy + (size_t)r * pld, 81 * sizeof(float));
         hv[r] = value[r];
     }
-    __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    const int per_copy = rows > 1 ? 1 : 0;  // k copies applied in order (the reference's call pattern)
-    EvalCache c = per_copy ? EvalCache{} : e->cache;
-    timed_launch(e, kKApply, k_apply, dim3(grid_waves(1)), dim3(kBlock), e->pool, e->tr, c, (const float *)hp,
-                 (int64_t)96, (const float *)hv, (int64_t)1,
-                 (const int32_t *)reinterpret_cast<int32_t *>(e->h_eval + e->h_eval_rows * 97), per_copy,
-                 bytes_ptr(e, kKApply));
-    int rc = check_launch();
-    if (rc) return rc;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // before the launch that reads them
+    e->host_apply_rows = rows;  // applied by the next k_flush1 (or flush_host_apply)
     e->phase = 1;
     e->n_pending = 0;
     return UTTT_OK;
@@ -2595,6 +2666,7 @@ static int check_tree_errors(uttt_engine *e) {
 int uttt_search_root_visits(uttt_engine_t *e, int32_t *visits, int32_t *n_legal) {
     if (!e) return UTTT_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = flush_host_apply(e)) return rc0;
     int rc = check_tree_errors(e);
     if (rc) return rc;
     const int n = e->tr.n_trees;
@@ -2611,6 +2683,7 @@ int uttt_search_root_visits(uttt_engine_t *e, int32_t *visits, int32_t *n_legal)
 int uttt_search_scores(uttt_engine_t *e, float temperature, float *scores, int32_t *n_legal) {
     if (!e) return UTTT_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = flush_host_apply(e)) return rc0;
     int rc = check_tree_errors(e);
     if (rc) return rc;
     const int n = e->tr.n_trees;
