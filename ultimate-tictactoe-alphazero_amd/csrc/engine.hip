@@ -208,10 +208,10 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction), in two
-// reductions of one instruction pair per step: the wave's largest value, then the smallest index among
-// the lanes holding it ("larger value, then smaller index": the reference's strict '>' scan in child
-// order). Values are never NaN here (the per-lane scan's strict '>' from -1e9 never takes one); -0 and
+// The same arg-max by DPP lane moves, no LDS round trips (k_select's per-level reduction): the wave's
+// largest value by one reduction of one instruction pair per step, then the smallest index among the
+// lanes holding it ("larger value, then smaller index": the reference's strict '>' scan in child order)
+// from one ballot when the maximum is unique, else from per-group ballots. Values are never NaN here (the per-lane scan's strict '>' from -1e9 never takes one); -0 and
 // +0 compare equal, so they tie on the index as in the scan. Each reduction runs within each row of 16
 // lanes (quad swaps, half-row and row mirrors), then row 0 into row 1 and row 2 into row 3
 // (row_bcast15), then row 1 into rows 2-3 (row_bcast31): the result is valid in lane 63.
@@ -233,12 +233,6 @@ UTTT_DPP_STEP(v_max_u32, hm)
 UTTT_DPP_STEP(v_max_u32, rm)
 UTTT_DPP_STEP(v_max_u32, b15)
 UTTT_DPP_STEP(v_max_u32, b31)
-UTTT_DPP_STEP(v_min_u32, q1)
-UTTT_DPP_STEP(v_min_u32, q2)
-UTTT_DPP_STEP(v_min_u32, hm)
-UTTT_DPP_STEP(v_min_u32, rm)
-UTTT_DPP_STEP(v_min_u32, b15)
-UTTT_DPP_STEP(v_min_u32, b31)
 // wave-uniform result: the index of the largest v, the lowest index among equal maxima
 __device__ __forceinline__ int wave_argmax(float v, int i) {
     // the value as an order-preserving unsigned (-0 canonicalised to +0 first), so each step of the max
@@ -257,15 +251,16 @@ __device__ __forceinline__ int wave_argmax(float v, int i) {
     // the usual case: one lane holds the maximum, and its index is the answer (no second pass)
     const uint64_t at = __ballot(b == top);
     if (__popcll(at) == 1) return __builtin_amdgcn_readlane(i, __builtin_ctzll(at));
-    uint32_t k = b == top ? (uint32_t)i : (uint32_t)kNone;  // indices are >= 0: unsigned min is the int min
-    v_min_u32_q1(k);
-    v_min_u32_q2(k);
-    v_min_u32_hm(k);
-    v_min_u32_rm(k);
-    v_min_u32_b15(k);
-    v_min_u32_b31(k);
-    asm volatile("s_nop 1");
-    return __builtin_amdgcn_readlane((int)k, 63);
+    // ties (a node expanded by a flush of k copies holds k equal children per action until they are
+    // visited): the smallest index among the lanes holding the maximum. Lane l's candidate is its own first
+    // maximum, child l + 64 g of its scan group g (i & 63 == l), so the answer is the lowest such lane of
+    // the lowest group present: one ballot per group from group 0 (round 5: in place of a second 6-step DPP
+    // reduction and its wait states; usually group 0 or 1 answers)
+    for (int g = 0; g < 64; ++g) {
+        const uint64_t m = __ballot(b == top && (i >> 6) == g);
+        if (m) return g * kWave + __builtin_ctzll(m);
+    }
+    return kNone;  // unreachable: some lane holds the maximum with a child index
 }
 
 // Orders this wave's global stores before its later global loads (other lanes
@@ -904,7 +899,10 @@ __device__ __forceinline__ void select_wave(Pool pool, Trees tr, EvalCache cache
                     trips += 2u + (unsigned int)((cnt + kWave - 1) / kWave);  // the node's record, the scan
                     // pv_mcts.py:120-130 under NumPy 2 promotion: float32 ops with sqrt(t)
                     // in double, or float64 throughout when the priors are float64;
-                    // np.argmax: first maximum, a NaN counts as the maximum.
+                    // np.argmax: first maximum, a NaN counts as the maximum. (k_apply refuses a
+                    // non-finite legal prior or value in both semantics, UTTT_ERR_NONFINITE, where
+                    // pv_mcts.py would keep searching, so no NaN statistic reaches this scan today;
+                    // the branch keeps the scan a complete restatement of np.argmax)
                     const bool p64 = (nm.x & kMetaP64) != 0u;
                     const double sqt = sqrt((double)total);
                     const float sq = (float)sqt;
