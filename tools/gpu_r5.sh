@@ -9,7 +9,8 @@
 #   pmcsel / pmctree  k_select / k_apply PMC traffic (headline / tree-only population)
 #   quick  headline + tree-only short bench lines    bench  bench.py (full: variants, isolated conv, CPU baselines)
 #   train  tools/bench_train.py   dptrain  tools/bench_train_dp.py (one nccl rank: eager DDP+SyncBN vs graphed DP step)
-#   vars   conv variants (diag lib)   lat  single-tree latency (Option A)   cycle  configs[4] on one GPU
+#   vars   conv variants (diag lib)   modes  conv MODE ablations (tools/diag/wino3h_modes.py)
+#     lat  single-tree latency (Option A)   cycle  configs[4] on one GPU
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -60,6 +61,8 @@ for s in $STEPS; do
     dptrain) timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
                --master-port 29531 tools/bench_train_dp.py --out $OUT/train_dp.json ${DPTRAIN_ARGS:-} > $OUT/train_dp.log 2>&1 ;;
     vars)  timeout -k 10 300 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
+    modes) MODES=${MODES:-0,8,1048576,1048584} timeout -k 10 300 python -u tools/diag/wino3h_modes.py ${MODE_BOARDS:-1344 16384} \
+             > $OUT/modes.log 2>&1 ;;
     lat)   timeout -k 10 300 python -u tools/diag/latency_single.py > $OUT/latency.log 2>&1 ;;
     cycle) timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle.json ${CYCLE_ARGS:-} > $OUT/cycle.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -49,11 +49,13 @@ def main(trace, bench_log, out):
         lines.append(f"| `{n}` | {a[0]} | {a[1] / 1e6:.2f} | {100 * a[1] / total:.2f} | {a[1] / a[0] / 1e3:.1f} | "
                      f"{a[2]} | {a[3]} | {a[4]} |")
     lines.append("")
+    seen = set()
     for key in ("roofline", "roofline_select", "roofline_backup"):
         rf = bench.get(key)
-        if not rf:
+        if not rf or rf["kernel"].split()[0] in seen:
             continue
         kname = rf["kernel"].split()[0]
+        seen.add(kname)
         sw = [r for r in win if kname in r[2]]
         avg = sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3
         if rf["unit"] == "TFLOP/s":
@@ -79,11 +81,13 @@ def main(trace, bench_log, out):
           "window_dispatches_k_select": nwin, "span_ms": span / 1e6, "busy_ms": total / 1e6,
           "kernels": {n: {"calls": a[0], "avg_us": a[1] / a[0] / 1e3, "total_ms": a[1] / 1e6} for n, a in agg.items()},
           "checks": {}}
+    seen = set()
     for key in ("roofline", "roofline_select", "roofline_backup"):
         rf = bench.get(key)
-        if not rf:
+        if not rf or rf["kernel"].split()[0] in seen:
             continue
         kname = rf["kernel"].split()[0]
+        seen.add(kname)
         sw = [r for r in win if kname in r[2]]
         js["checks"][key] = {"kernel": kname, "rocprof_avg_us": sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3,
                              "rocprof_dispatches": len(sw), "event_avg_us": rf["avg_launch_us"],
