@@ -43,6 +43,7 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
             case 131072: ablation_res<131072>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
             case 196608: ablation_res<196608>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
             case 8: ablation_res<8>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case kResEarly: ablation_res<kResEarly>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
             default: ablation_res<0>(x, u, u_scale, bias, y, x_amax, n_boards, st);
         }
         return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;

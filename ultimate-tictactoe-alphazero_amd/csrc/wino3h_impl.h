@@ -66,6 +66,7 @@ constexpr int kFoldAT = 1 << 18;          // the fold along u by A^T itself (rou
 constexpr int kEpiBarrier = 1 << 7;       // a set's epilogue starts after every wave's last point GEMMs (a barrier):
                                           // the earlier waves' epilogue VALU no longer takes the issue slots of
                                           // their SIMD partners' last point GEMMs
+constexpr int kResEarly = 1 << 11;        // residual form: both tile blocks' residual loads issued at the epilogue's start
 constexpr int kEpiPrio = 1 << 10;         // ... instead: waves 4-7 run a set's last point loop at s_setprio 1
 constexpr int kEarlyLoad = 1 << 19;       // the chunk-after-next's inputs requested at the end of this chunk's
                                           // point GEMMs (before the barrier the earlier waves wait at), except
@@ -532,6 +533,17 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
         // this tile's board's V scale times su: both powers of two, so 1/x is exact
         inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
     }
+    // kResEarly (diagnostic): every residual load of the set's epilogue in flight before Y is formed
+    floatx4 rve[2][9];
+    if constexpr (RES && (MODE & kResEarly)) {
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab) {
+                rve[rt][ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+                if (live[rt]) rve[rt][ab] = *reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+            }
+    }
     if constexpr (!(MODE & kFoldAT)) {  // S = Z^-1 S': rows 0 and 2 get row 1 added (both tile blocks)
 #pragma unroll
         for (int v = 0; v < 5; ++v)
@@ -546,7 +558,10 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
         float vmax = 0.0f;
         // tile block rt: residual loads first (in flight while Y is formed)
         floatx4 rv[9];
-        if constexpr (RES) {
+        if constexpr (RES && (MODE & kResEarly)) {
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab) rv[ab] = rve[rt][ab];
+        } else if constexpr (RES) {
 #pragma unroll
             for (int ab = 0; ab < 9; ++ab) {
                 rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
