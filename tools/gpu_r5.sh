@@ -60,7 +60,7 @@ for s in $STEPS; do
     train) timeout -k 10 400 python -u tools/bench_train.py ${TRAIN_ARGS:-} > $OUT/train.log 2>&1 ;;
     dptrain) timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
                --master-port 29531 tools/bench_train_dp.py --out $OUT/train_dp.json ${DPTRAIN_ARGS:-} > $OUT/train_dp.log 2>&1 ;;
-    vars)  timeout -k 10 300 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
+    vars)  timeout -k 10 400 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
     modes) MODES=${MODES:-0,8,1048576,1048584} timeout -k 10 300 python -u tools/diag/wino3h_modes.py ${MODE_BOARDS:-1344 16384} \
              > $OUT/modes.log 2>&1 ;;
     lat)   timeout -k 10 300 python -u tools/diag/latency_single.py > $OUT/latency.log 2>&1 ;;

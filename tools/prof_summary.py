@@ -64,8 +64,9 @@ def main(trace, bench_log, out):
         else:
             work = rf["algo_bytes_per_launch"]
             rate = f"{work / (avg * 1e3):.2f} GB/s algorithmic (rocprof time)"
+        ev = rf.get("event_avg_launch_us", rf["avg_launch_us"])
         lines.append(f"- `{kname}` in window: {len(sw)} dispatches, avg {avg:.1f} us (rocprof) vs "
-                     f"{rf['avg_launch_us']} us (bench HIP events, {rf['launches']} launches) -> {rate}")
+                     f"{ev} us (this run's dispatch events, under the profiler; {rf['launches']} launches) -> {rate}")
     with open(out, "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
@@ -90,7 +91,7 @@ def main(trace, bench_log, out):
         seen.add(kname)
         sw = [r for r in win if kname in r[2]]
         js["checks"][key] = {"kernel": kname, "rocprof_avg_us": sum(e - s for s, e, *_ in sw) / max(len(sw), 1) / 1e3,
-                             "rocprof_dispatches": len(sw), "event_avg_us": rf["avg_launch_us"],
+                             "rocprof_dispatches": len(sw), "event_avg_us": rf.get("event_avg_launch_us", rf["avg_launch_us"]),
                              "event_launches": rf["launches"]}
     with open(out.rsplit(".", 1)[0] + ".json", "w") as f:
         json.dump(js, f, indent=1)

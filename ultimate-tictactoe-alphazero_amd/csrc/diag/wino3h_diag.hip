@@ -44,6 +44,10 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
             case 196608: ablation_res<196608>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
             case 8: ablation_res<8>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
             case kResEarly: ablation_res<kResEarly>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case kEpiOrder: ablation_res<kEpiOrder>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case kEpiLoad: ablation_res<kEpiLoad>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case kEpiNT: ablation_res<kEpiNT>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
+            case kEpiOrder | kEpiLoad: ablation_res<kEpiOrder | kEpiLoad>(x, u, u_scale, bias, y, x_amax, n_boards, st); break;
             default: ablation_res<0>(x, u, u_scale, bias, y, x_amax, n_boards, st);
         }
         return hipGetLastError() == hipSuccess ? UTTT_OK : UTTT_ERR_HIP;
@@ -59,6 +63,10 @@ int uttt_diag_wino3h_ablation(const float *x, const uint16_t *u, float u_scale, 
         case 49: hipLaunchKernelGGL((k_wino3h_conv<false, 49>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
         case 112: hipLaunchKernelGGL((k_wino3h_conv<false, 112>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
         case 256: hipLaunchKernelGGL((k_wino3h_conv<false, 256>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case kEpiOrder: hipLaunchKernelGGL((k_wino3h_conv<false, kEpiOrder>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case kEpiLoad: hipLaunchKernelGGL((k_wino3h_conv<false, kEpiLoad>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case kEpiNT: hipLaunchKernelGGL((k_wino3h_conv<false, kEpiNT>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
+        case kEpiOrder | kEpiLoad: hipLaunchKernelGGL((k_wino3h_conv<false, kEpiOrder | kEpiLoad>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
         case 8: hipLaunchKernelGGL((k_wino3h_conv<false, 8>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
         case 4: hipLaunchKernelGGL((k_wino3h_conv<false, 4>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
         case 12: hipLaunchKernelGGL((k_wino3h_conv<false, 12>), grid, dim3(NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax, 0, nullptr, nullptr, 0, n_boards, (const int32_t *)nullptr); break;
@@ -131,6 +139,9 @@ int uttt_diag_wino3h_variant(const float *x, const uint16_t *u, float u_scale, c
         case 76: UTTT_V(kEarlyLoad, 3); break;
         case 77: UTTT_V(kEarlyLoad | kBufferX, 3); break;
         case 78: UTTT_V(kEpiBarrier, 3); break;
+        case 81: UTTT_V(kEpiOrder, 3); break;  // the branch-free ordered epilogue (round 5 A/B)
+        case 82: UTTT_V(kEpiNT, 3); break;
+        case 83: UTTT_V(kEpiLoad, 3); break;
         case 79: UTTT_V(kEpiPrio, 3); break;
         case 80: UTTT_V(kEpiBarrier | kEarlyLoad, 3); break;
         case 71: UTTT_V(kBufferX, 3); break;

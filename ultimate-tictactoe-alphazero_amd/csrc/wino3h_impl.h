@@ -20,6 +20,7 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef float floatx8 __attribute__((ext_vector_type(8)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 constexpr int C = 128;        // channels in and out
 constexpr int NP = 25;        // transform points
@@ -66,6 +67,10 @@ constexpr int kFoldAT = 1 << 18;          // the fold along u by A^T itself (rou
 constexpr int kEpiBarrier = 1 << 7;       // a set's epilogue starts after every wave's last point GEMMs (a barrier):
                                           // the earlier waves' epilogue VALU no longer takes the issue slots of
                                           // their SIMD partners' last point GEMMs
+constexpr int kEpiOrder = 1 << 12;        // epilogue by branch-free buffer loads / stores, tile block 1's residual requested
+                                           // before block 0's stores (round 5: same bits, 1-5% slower than the product)
+constexpr int kEpiLoad = 1 << 14;
+constexpr int kEpiNT = 1 << 15;            // kEpiOrder with nontemporal output stores          // the next set's second chunk's inputs requested before the epilogue's stores
 constexpr int kResEarly = 1 << 11;        // residual form: both tile blocks' residual loads issued at the epilogue's start
 constexpr int kEpiPrio = 1 << 10;         // ... instead: waves 4-7 run a set's last point loop at s_setprio 1
 constexpr int kEarlyLoad = 1 << 19;       // the chunk-after-next's inputs requested at the end of this chunk's
@@ -553,6 +558,77 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
                 S[10 + v].p[j] = S[10 + v].p[j] + S[5 + v].p[j];
             }
     }
+    if constexpr (MODE & (kEpiOrder | kEpiNT)) {
+        // Diagnostic (round 5): branch-free buffer loads and stores, a dead tile's (the empty slot, a board
+        // past the end) at an offset past the buffer (loads return 0, stores are dropped), so the compiler
+        // counts them exactly, and tile block 1's residual requested before block 0's stores, so its wait
+        // does not include them (vmcnt counts loads and stores in one counter). Same bits as the product;
+        // interleaved A/B 1-5% slower, so the product keeps the form below.
+        // dead offset 0xFFF00000: plus the largest position offset (20 x 512 B) it stays past the range
+        const uint32_t nbytes = (uint32_t)min((size_t)n_boards * 81 * C * 4, (size_t)0xFFE00000u);
+        const rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(y, 0, (int)nbytes, 0x00020000);
+        const rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(res ? res : y), 0, (int)nbytes, 0x00020000);
+        uint32_t vo[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) vo[rt] = live[rt] ? (uint32_t)(off[rt] * 4) : 0xFFF00000u;
+        auto rload = [&](int rt, floatx4 (&rv)[9]) {
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab)
+                rv[ab] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rr, vo[rt] + ((ab / 3) * 9 + ab % 3) * C * 4, 0, 0));
+        };
+        floatx4 rv[9];
+        if constexpr (RES) rload(0, rv);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            floatx4 out[9];
+            float vmax = 0.0f;
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab) {
+                const int a = ab / 3, b = ab % 3;
+                floatx4 acc = {};
+#pragma unroll
+                for (int v = 0; v < 5; ++v) {
+                    if (at(b, v) == 0) continue;
+                    const Acc &q = S[a * 5 + v];
+                    const floatx4 s4 = {q.p[2 * rt].x, q.p[2 * rt].y, q.p[2 * rt + 1].x, q.p[2 * rt + 1].y};
+                    acc = at(b, v) == 1 ? acc + s4
+                        : at(b, v) == -1 ? acc - s4
+                                         : __builtin_elementwise_fma(floatx4((float)at(b, v)), s4, acc);
+                }
+                floatx4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = __builtin_fmaf(acc[r], inv[rt], bb4[r]);
+                if constexpr (RES) o += rv[ab];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = fmaxf(o[r], 0.0f);
+                out[ab] = o;
+                vmax = fmaxf(vmax, fmaxf(fmaxf(o[0], o[1]), fmaxf(o[2], o[3])));
+            }
+#pragma unroll
+            for (int i = 0; i < 15; ++i) {
+                S[i].p[2 * rt] = floatx2{0.0f, 0.0f};
+                S[i].p[2 * rt + 1] = floatx2{0.0f, 0.0f};
+            }
+            if constexpr (RES)
+                if (rt == 0) rload(1, rv);  // in flight under block 0's stores
+#pragma unroll
+            for (int ab = 0; ab < 9; ++ab)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, out[ab]), yr,
+                                                       vo[rt] + ((ab / 3) * 9 + ab % 3) * C * 4, 0,
+                                                       (MODE & kEpiNT) ? 2 : 0);
+            if (y_amax) {
+                vmax = live[rt] ? vmax : 0.0f;
+                vmax = fmaxf(vmax, __shfl_xor(vmax, 16));
+                vmax = fmaxf(vmax, __shfl_xor(vmax, 32));
+                if (el < 16 && live[rt]) {
+                    if (s_bmax) atomicMax(s_bmax + (board_of[rt] - (GB * (grp) + 3 * h)), __builtin_bit_cast(uint32_t, vmax));
+                    else atomicMax(y_amax + board_of[rt], __builtin_bit_cast(uint32_t, vmax));
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
         float vmax = 0.0f;
@@ -756,7 +832,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         // the next chunk's inputs load during this chunk's transform (registers are
         // free then; the point loop needs nearly all of them)
         if (!(MODE & kEarlyLoad) || g == 0 || c == 0)
-            if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
+            if (!((MODE & kEpiLoad) && c == 0 && g > 0))  // kEpiLoad: requested before the last epilogue
+                if (g + 1 < G) load_x<MODE>(xr, x, set_b0(g + 1), n_boards, chunk_of(g + 1), fresh(tid));
         // the next chunk's V scales: this set's, or the next set's after its last chunk
         SetScale sc_next = sc;
         if (c == NCH - 1 && g + 1 < G) sc_next = set_scale(x_amax, x_amax_per_board, set_b0(g + 1), n_boards);
@@ -783,6 +860,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         mark(g, 3, t0);
         if constexpr (MODE & kEarlyLoad)
             if (c != NCH - 1 && g + 2 < G) load_x<MODE>(xr, x, set_b0(g + 2), n_boards, chunk_of(g + 2), fresh(tid));
+        if constexpr (MODE & kEpiLoad)
+            if (c == NCH - 1 && g + 2 < G) load_x<MODE>(xr, x, set_b0(g + 2), n_boards, chunk_of(g + 2), fresh(tid));
         if (c == NCH - 1)
             set_epilogue<RES, MODE>(S, set_of(g), sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, 0, s_bmax);
         sc = sc_next;
