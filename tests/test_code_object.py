@@ -22,6 +22,8 @@ PRODUCT = {
     "k_scan": "6k_scanE",
     "k_move_end": "10k_move_endE",
     "k_finalize": "10k_finalizeE",
+    "k_archive": "9k_archiveE",
+    "k_flush1<cpp>": "8k_flush1ILb0E",
     "k_stem": "6k_stemE",
     "k_heads": "7k_headsE",
 }

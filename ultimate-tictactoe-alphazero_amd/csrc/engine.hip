@@ -1565,12 +1565,6 @@ struct SelfPlay {
 
 // numpy legacy RandomState: init_genrand(seed) (mt19937_seed), genrand_int32
 // with the standard twist/tempering, random_sample = 53-bit double of 2 draws.
-__device__ void mt_seed(uint32_t *key, int32_t *pos, uint32_t seed) {
-    key[0] = seed;
-    for (int i = 1; i < 624; ++i) key[i] = 1812433253u * (key[i - 1] ^ (key[i - 1] >> 30)) + (uint32_t)i;
-    *pos = 624;
-}
-
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
     y ^= (y << 7) & 0x9d2c5680u;
@@ -1824,10 +1818,17 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
     const int tid = threadIdx.x;
     const int per = (sp.slots + 1023) / 1024;
     const int b = tid * per, e = min(b + per, sp.slots);
+    // up to kFinPer slots per thread (4,096 slots) are read once, all loads in flight together, and
+    // kept in registers for the second pass; more slots per thread are re-read there
+    constexpr int kFinPer = 4;
+    Slot held[kFinPer];
+#pragma unroll
+    for (int j = 0; j < kFinPer; ++j)
+        if (b + j < e) held[j] = sp.slot[b + j];
     long long fl = 0;
     int fr = 0, fc = 0;
     for (int i = b; i < e; ++i) {
-        const Slot &sl = sp.slot[i];
+        const Slot sl = i - b < kFinPer ? held[i - b] : sp.slot[i];
         if (sl.finished) {
             fl += sl.fin_len;
             ++fc;
@@ -1846,7 +1847,7 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
     const long long fin_total = (long long)fl_tot;
     const int free_total = (int)(cnt_tot & 0xFFFFFFFFull), fin_count = (int)(cnt_tot >> 32);
     for (int i = b; i < e; ++i) {
-        Slot sl = sp.slot[i];
+        Slot sl = i - b < kFinPer ? held[i - b] : sp.slot[i];
         if (sl.finished) {
             if (off + sl.fin_len <= sp.arena_cap && gi < sp.games_cap) {
                 sl.fin_offset = off;
@@ -1901,25 +1902,53 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
 // Copy each just-finished game's plies to its arena rows, with values
 // (self_play_cpp.py:95-99: ply 0 gets the final value, then alternating), and seed the MT19937
 // key of a slot k_finalize gave a new game (numpy's init_genrand(seed_base + game)).
-__global__ void k_archive(SelfPlay sp, const unsigned long long *err) {
+// The seeding wave runs init_genrand's 624-step chain uniformly (every lane the same values, wave-uniform
+// operands) and lane i & 63 keeps step i: ten coalesced 64-word stores instead of 624 one-lane stores.
+__device__ __forceinline__ void mt_seed_wave(uint32_t *key, int32_t *pos, uint32_t seed) {
+    const int lane = lane_id();
+    uint32_t x = seed, mine = seed;
+    for (int i0 = 0; i0 < 624; i0 += kWave) {
+        const int n = min(kWave, 624 - i0);
+        for (int j = 0; j < n; ++j) {
+            const int i = i0 + j;
+            if (i > 0) x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+            mine = lane == j ? x : mine;
+        }
+        if (lane < n) key[i0 + lane] = mine;
+    }
+    if (lane == 0) *pos = 624;
+}
+
+// Each block: one slot. The last wave seeds a refilled slot's key while the others copy a finished game's
+// plies, eight independent loads in flight per thread before their stores (the copy was one dependent
+// load-store pair per iteration: ~19 memory round trips per game, round 4's 39 us launch).
+__global__ __launch_bounds__(256) void k_archive(SelfPlay sp, const unsigned long long *err) {
     if (err && *err != ~0ull) return;
     const int s = blockIdx.x;
-    const Slot &sl = sp.slot[s];
-    if (sl.seed_pending && threadIdx.x == 0) {
-        mt_seed(sp.mt_key + (size_t)s * 624, sp.mt_pos + s, sp.seed_base + (uint32_t)sl.game);
-        sp.slot[s].seed_pending = 0;
+    const Slot sl = sp.slot[s];
+    const int wave = (int)threadIdx.x >> 6;
+    if (sl.seed_pending && wave == 3) {
+        mt_seed_wave(sp.mt_key + (size_t)s * 624, sp.mt_pos + s, sp.seed_base + (uint32_t)sl.game);
+        if (lane_id() == 0) sp.slot[s].seed_pending = 0;
     }
     if (!sl.finished || sl.fin_offset < 0) return;
-    for (int i = threadIdx.x; i < sl.fin_len * 81; i += blockDim.x) {
-        const int ply = i / 81, a = i % 81;
-        const size_t src = (size_t)s * kMaxPlies + ply;
-        const size_t dst = (size_t)sl.fin_offset + ply;
-        sp.ar_policy[dst * 81 + a] = sp.ply_policy[src * 81 + a];
-        if (a == 0) {
-            sp.ar_state[dst] = sp.ply_state[src];
-            sp.ar_action[dst] = sp.ply_action[src];
-            sp.ar_value[dst] = (int8_t)((ply & 1) ? -sl.fin_value : sl.fin_value);
-        }
+    const size_t src0 = (size_t)s * kMaxPlies, dst0 = (size_t)sl.fin_offset;
+    const double *__restrict__ from = sp.ply_policy + src0 * 81;
+    double *__restrict__ to = sp.ar_policy + dst0 * 81;
+    const int n = sl.fin_len * 81;  // the game's policy rows are contiguous in both places
+    constexpr int kU = 8;
+    for (int i0 = threadIdx.x; i0 < n; i0 += 256 * kU) {
+        double v[kU];
+#pragma unroll
+        for (int j = 0; j < kU; ++j) v[j] = i0 + 256 * j < n ? from[i0 + 256 * j] : 0.0;
+#pragma unroll
+        for (int j = 0; j < kU; ++j)
+            if (i0 + 256 * j < n) to[i0 + 256 * j] = v[j];
+    }
+    for (int ply = threadIdx.x; ply < sl.fin_len; ply += 256) {
+        sp.ar_state[dst0 + ply] = sp.ply_state[src0 + ply];
+        sp.ar_action[dst0 + ply] = sp.ply_action[src0 + ply];
+        sp.ar_value[dst0 + ply] = (int8_t)((ply & 1) ? -sl.fin_value : sl.fin_value);
     }
 }
 
