@@ -36,9 +36,10 @@ F16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF den
 NETCAL = os.path.join(REPO, "tests", "golden", "netcal.npz")
 
 # residual-tower conv, per board: MFMA flops the kernels issue, and the direct 3x3 conv's flops
-CONV_EXEC_FLOP = {"wino3h": 3 * 9 * 25 * 128 * 128 * 2}  # F(3x3,3x3): 9 tiles x 25 points, 3 f16 products
+CONV_EXEC_FLOP = {"wino3h": 3 * 9 * 25 * 128 * 128 * 2,  # F(3x3,3x3): 9 tiles x 25 points, 3 f16 products
+                  "wino3h_f16": 9 * 25 * 128 * 128 * 2}   # the f16 mode: one product
 CONV_DIRECT_FLOP = 2 * 81 * 128 * 1152
-CONV_PEAK = {"wino3h": F16_DENSE_PEAK_TFLOPS}
+CONV_PEAK = {"wino3h": F16_DENSE_PEAK_TFLOPS, "wino3h_f16": F16_DENSE_PEAK_TFLOPS}
 # residual-tower conv, algorithmic HBM bytes per board: read x, write y (+ read the residual on
 # every second conv); the transformed weights (1.6 MB) are read once per launch, L2/MALL-resident
 CONV_BYTES_PER_BOARD = 81 * 128 * 4 * 2.5
@@ -62,7 +63,9 @@ def parse():
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--batch", type=int, default=8, help="MCTS_BATCH_SIZE (per-tree flush size)")
-    ap.add_argument("--evaluator", choices=["fused", "nn", "hash"], default="fused")
+    ap.add_argument("--evaluator", choices=["fused", "nn", "hash", "fused_f16"], default="fused",
+                    help="fused: the HIP network at f32-level accuracy (the measurement); fused_f16: its optional "
+                         "one-product f16 mode (not the reference's numerics; a variant line only)")
     ap.add_argument("--net", choices=["seed0", "calibrated"], default="seed0",
                     help="seed0: the reference's initial best.pth; calibrated: tests/golden/netcal.npz")
     ap.add_argument("--age", type=int, default=300,
@@ -217,13 +220,13 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     dev = torch.device("cuda", local)
     sp = SelfPlay(games, sims, batch, 1.0, device=local, cache_log2=cache_log2, lanes=lanes,
                   cache_clear_every=cache_clear_every)
-    conv = {"fused": "wino3h"}.get(evaluator)
+    conv = {"fused": "wino3h", "fused_f16": "wino3h"}.get(evaluator)
     tower_events = []
     if evaluator == "hash":
         make_inner = HashEvaluator
     elif conv:
         def make_inner(eng):
-            fe = FusedNetworkEvaluator(net, eng, conv=conv)
+            fe = FusedNetworkEvaluator(net, eng, conv=conv, precision="f16" if evaluator == "fused_f16" else "f32")
             fe.tower_events = tower_events
             return fe
     else:
@@ -287,7 +290,8 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
         n_rows, nn_ms, nn_sum = sum(int(n) for n in rows), union_ms(ivs), sum(hi - lo for lo, hi in ivs)
     out = {"sims": done, "elapsed": elapsed, "rows": n_rows, "nn_ms": nn_ms,
            "nn_lane_sum_ms": nn_sum, "tower": tower, "stats": st,
-           "rounds": sp.rounds - rounds0, "finished": sp.finished - finished0, "conv": conv,
+           "rounds": sp.rounds - rounds0, "finished": sp.finished - finished0,
+           "conv": "wino3h_f16" if evaluator == "fused_f16" else conv,
            "cache": sp.cache_stats() if cache_log2 else None, "trees_per_launch": games // lanes}
     del sp
     torch.cuda.empty_cache()
@@ -326,7 +330,7 @@ def conv_roofline(r, steps):
     achieved = flop / (avg_us * 1e-6) / 1e12
     pmc = newest_profile("pmc_conv.json", {"kernel": "k_wino3h_conv"}) if conv == "wino3h" else None
     traffic = round(pmc["hbm_bytes_per_board"] * boards_per_launch) if pmc else None
-    algo_bytes = CONV_BYTES_PER_BOARD * boards_per_launch + U_BYTES_PER_SET
+    algo_bytes = CONV_BYTES_PER_BOARD * boards_per_launch + U_BYTES_PER_SET // (2 if conv == "wino3h_f16" else 1)
     return {"kernel": f"k_{conv}_conv (residual-tower 3x3 conv, Winograd F(3x3,3x3) on the "
                       f"{'f16 MFMA, 3-term split-f16 products, f32 accumulation' if conv == 'wino3h' else 'f32 MFMA'})",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": CONV_PEAK[conv], "unit": "TFLOP/s",
@@ -343,7 +347,8 @@ def conv_roofline(r, steps):
             "avg_launch_us": round(avg_us, 2), "launches": launches, "boards_per_launch": round(boards_per_launch, 1),
             "executed_flop_per_board": CONV_EXEC_FLOP[conv], "direct_equiv_flop_per_board": CONV_DIRECT_FLOP,
             "direct_equiv_tflops": round(CONV_DIRECT_FLOP * boards_per_launch / (avg_us * 1e-6) / 1e12, 1),
-            "vmem_stream": conv_vmem_roofline(r["tower"], avg_us, r["nn_ms"]),
+            "vmem_stream": conv_vmem_roofline(r["tower"], avg_us, r["nn_ms"],
+                                              U_BYTES_PER_SET // (2 if conv == "wino3h_f16" else 1)),
             "note": "two lanes' conv launches overlap on the GPU, so each launch's duration includes the time it "
                     "shares the CUs with the other lane's; aggregate = nn.mfma_executed_tflops"}
 
@@ -407,12 +412,12 @@ def conv_sets(n):
     return 2 * (n // 7) + (0 if n % 7 == 0 else (1 if n % 7 <= 3 else 2))
 
 
-def conv_vmem_roofline(tower, avg_us, nn_ms):
+def conv_vmem_roofline(tower, avg_us, nn_ms, u_bytes=U_BYTES_PER_SET):
     """The conv's binding resource: bytes through each CU's vector-memory path per launch (U once
     per set, inputs, outputs and residual per board) / launch time, against the measured ceiling.
     aggregate_*: every conv's bytes over the union of the lanes' forward intervals (stem and heads
     included, so conservative) -- the rate the chip sustains while two lanes' launches overlap."""
-    per_fwd = [conv_sets(n) * U_BYTES_PER_SET + CONV_BYTES_PER_BOARD * n for n, _ in tower]
+    per_fwd = [conv_sets(n) * u_bytes + CONV_BYTES_PER_BOARD * n for n, _ in tower]
     per_launch = sum(per_fwd) / len(tower)
     achieved = per_launch / (avg_us * 1e-6) / 1e12
     agg = 32 * sum(per_fwd) / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
@@ -549,6 +554,10 @@ def main():
                         # one lane: with no network to overlap, one launch per round over every tree is the
                         # fastest shape (1 / 2 / 4 lanes: 170.6M / 141M / 82M sims/s, profiles/r3/ab/hashlanes.log)
                         ("tree_only_4096x50", dict(evaluator="hash", age=100, lanes=1)),
+                        # SURVEY §8(f) rank 1's optional fast evaluator: the tower conv with one f16 product per
+                        # point (uttt_nn_conv3x3_wino3h_f16, ~1e-3 relative): not the reference's numerics, so a
+                        # variant line beside the f32-level headline, never the headline
+                        ("f16_mode", dict(evaluator="fused_f16")),
                         ("tree_only_4096x400", dict(evaluator="hash", sims=400, age=30, warmup=2, steps=4, lanes=1))):
             cfg = dict(net=net0, games=G, sims=S, batch=B, lanes=args.lanes, cache_log2=args.cache_log2,
                        age=args.age, warmup=3, steps=10, evaluator=args.evaluator)
@@ -580,6 +589,8 @@ def main():
                 sv["breakdown_ms"]["wall"] = round(rv["elapsed"] * 1e3, 2)
                 sv["note"] = ("hash evaluator in place of the network: the search kernels' own rate, to set beside "
                               "cpu_baselines.b_tree_all_cores (the reference's C++ search with the same evaluator)")
+            elif cfg["evaluator"] == "fused_f16":
+                sv["precision"] = "f16: one f16 MFMA product per Winograd point (not f32-level; DESIGN.md §5)"
             else:
                 cr = conv_roofline(rv, cfg["steps"]) or {}
                 sv["conv_roofline_frac"] = cr.get("frac")
@@ -621,6 +632,8 @@ def main():
             "vs_baseline": None,
             "dtype": {"fused": "f32 activations and accumulation; tower point GEMMs as 3-term split-f16 products "
                                "on the f16 MFMA (f32-level accuracy: within 1e-5 of the reference's fp32 network)",
+                      "fused_f16": "f32 activations and accumulation; tower point GEMMs as ONE f16 product (the "
+                                   "optional f16 mode: ~1e-2 on the network's outputs, not the reference's numerics)",
                       "nn": "f32", "hash": "f32 (hash evaluator)"}[args.evaluator],
             "data": "synthetic: self-play from the initial position, games refilled as they end; DualNetwork "
                     + ("random init torch.manual_seed(0) (the reference's initial best.pth)" if args.net == "seed0"
@@ -635,6 +648,9 @@ def main():
                 "evaluator": {"fused": "DualNetwork 128f x16 on HIP kernels: stem from bitboards, residual tower as "
                                        "fused Winograd F(3x3,3x3) convs (csrc/wino3h_conv.hip, split-f16 MFMA, f32 "
                                        "accumulation, per-board scaling), heads (csrc/nn_kernels.hip)",
+                              "fused_f16": "DualNetwork 128f x16 on HIP kernels in the optional f16 mode: the "
+                                           "Winograd tower conv with one f16 MFMA product per point "
+                                           "(uttt_nn_conv3x3_wino3h_f16)",
                               "nn": "DualNetwork 128f x16 fp32, BN folded, PyTorch-ROCm/MIOpen",
                               "hash": "device hash evaluator (no network)"}[args.evaluator],
                 "parallelism": f"games sharded over {world} GPU(s) by contiguous global-id blocks, "

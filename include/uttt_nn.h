@@ -76,6 +76,18 @@ int uttt_nn_conv3x3_wino3h_dev(const float *x, const uint16_t *u, float u_scale,
                                const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
                                uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
                                int32_t max_boards, void *stream);
+/* f16 mode (not f32-level; the optional fast evaluator of SURVEY §8(f) rank 1): the same conv with
+ * M = Vhi Uhi alone (one f16 MFMA product instead of three, U's hi plane only), the same u buffer,
+ * scales and argument meaning. Outputs within ~1e-3 relative of the f32 conv; a board's
+ * outputs still depend on its own inputs only. */
+int uttt_nn_conv3x3_wino3h_f16(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                               const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                               uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, int32_t n_boards,
+                               void *stream);
+int uttt_nn_conv3x3_wino3h_f16_dev(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                                   const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                                   uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
+                                   int32_t max_boards, void *stream);
 /* Small batches: the conv's 128 output channels split over 2 workgroups per set (same output bits
  * as the persistent kernel). split: -1 automatic (default: up to 28 boards), 0 or 1 never, 2 always. */
 int uttt_nn_wino3h_set_split(int32_t split);

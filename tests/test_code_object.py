@@ -16,6 +16,8 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 PRODUCT = {
     "k_wino3h_conv<residual>": "k_wino3h_convILb1ELi0ELi3E",
     "k_wino3h_conv<plain>": "k_wino3h_convILb0ELi0ELi3E",
+    "k_wino3h_conv<residual, f16>": "k_wino3h_convILb1ELin2147483648ELi3E",
+    "k_wino3h_conv<plain, f16>": "k_wino3h_convILb0ELin2147483648ELi3E",
     "k_select<cpp>": "8k_selectILb0E",
     "k_select<py>": "8k_selectILb1E",
     "k_apply": "7k_applyE",

@@ -901,3 +901,70 @@ def test_train_network_runs_on_gpu(gpu):
     losses = train.train_network(model, hist, epochs=6, batch_size=64, device=torch.device("cuda", 0), log=None)
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
     DualNetwork().load_state_dict(model.state_dict())
+
+
+def test_f16_mode_conv_error_and_batch_independence(gpu):
+    """The conv's optional f16 mode (uttt_nn_conv3x3_wino3h_f16: M = Vhi Uhi, one f16 MFMA product per point,
+    SURVEY §8(f) rank 1's fast evaluator) against an f64 direct conv: within 5e-3 of each board's output scale
+    (measured 1.7e-3 .. 3.8e-3, tools/diag/f16_mode_check.py; the product's split-f16 form: 1-2e-6), the
+    per-board max row exact, different from the product's bits, and a board's outputs independent of the
+    batch it is in."""
+    import torch
+    import torch.nn.functional as F
+    from uttt_amd.model import fold_bn, random_network
+    from uttt_amd.nnfast import conv3x3_wino3h, wino3h_weights
+    net = random_network(3)
+    g = torch.Generator().manual_seed(4)
+    for blk_i, n, scale in ((5, 1, 1.0), (3, 9, 1e-3), (15, 30, 1e3), (9, 700, 1.0)):
+        w, b = fold_bn(net.residual_blocks[blk_i].conv1, net.residual_blocks[blk_i].bn1)
+        u, su = wino3h_weights(w)
+        u, w, b = u.cuda(), w.cuda(), b.cuda()
+        x = (torch.relu(torch.randn(n, 81, 128, generator=g)) * scale).cuda()
+        r = (torch.randn(n, 81, 128, generator=g) * scale).cuda()
+        ref = F.conv2d(x.reshape(n, 9, 9, 128).permute(0, 3, 1, 2).double(), w.double(), b.double(),
+                       padding=1).permute(0, 2, 3, 1).reshape(n, 81, 128)
+        for res in (None, r):
+            ya = torch.zeros(n, dtype=torch.int32, device="cuda")
+            y = conv3x3_wino3h(x, u, su, b, res, y_amax=ya, precision="f16")
+            want = torch.relu(ref + (res.double() if res is not None else 0)).float()
+            err = (y - want).abs().reshape(n, -1).amax(dim=1) / want.abs().reshape(n, -1).amax(dim=1).clamp_min(1e-30)
+            assert err.max().item() <= 5e-3, (blk_i, n, res is None, err.max().item())
+            assert torch.equal(ya.view(torch.float32), y.reshape(n, -1).amax(dim=1))
+            assert not torch.equal(y, conv3x3_wino3h(x, u, su, b, res))  # it is not the product's form
+            k = min(n, 5)
+            yk = conv3x3_wino3h(x[:k].contiguous(), u, su, b, res[:k].contiguous() if res is not None else None,
+                                precision="f16")
+            assert torch.equal(y[:k], yk)
+
+
+def test_f16_mode_evaluator_and_search(gpu, oracle_lib):
+    """FusedNetworkEvaluator(precision="f16") on search leaves: the calibrated net's value and post-softmax
+    policy within 3e-2 of the fp32 DualNetwork (measured 1.6e-2 / 1.4e-2 on 400 positions), and a self-play
+    move through it completes with legal, normalised scores. The f32-level evaluator stays the default; the
+    f16 mode is opt-in (precision="f16" or UTTT_NN_PRECISION=f16)."""
+    import torch
+    from uttt_amd.model import calibrated_network, policy_logits
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    roots, _ = _random_positions(oracle_lib, 200, seed=21)
+    bs = gpu.BatchedSearch(len(roots), 50)
+    e = bs.engine
+    e.use_stream()
+    net, cpu = calibrated_network(NETCAL, "cuda"), calibrated_network(NETCAL, "cpu")
+    fused = FusedNetworkEvaluator(net, e, precision="f16")
+    assert FusedNetworkEvaluator(net, e).precision == "f32"
+    e.search_begin(roots, 50, 8)
+    for _ in range(3):
+        n = e.select(bs.x)
+        p, v = fused.forward(n, softmax=True)
+        z_cpu, v_cpu = policy_logits(cpu, bs.x[:n].cpu())
+        assert (v.cpu() - v_cpu.reshape(-1)).abs().max().item() <= 3e-2
+        assert (p.cpu() - torch.softmax(z_cpu, dim=1)).abs().max().item() <= 3e-2
+        assert torch.allclose(p.sum(dim=1).cpu(), torch.ones(n), atol=1e-5)
+        e.apply(p, v)
+    sp = gpu.SelfPlay(64, 50, 8, 1.0)
+    sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng, precision="f16"))
+    sp.run(0, 8, 11)
+    plies = gpu.history_from_records(sp.records())
+    assert len(plies) > 0
+    for x, pol, val in plies:
+        assert abs(sum(pol) - 1.0) < 1e-6 and val in (-1, 0, 1)

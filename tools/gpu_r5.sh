@@ -10,7 +10,7 @@
 #   quick  headline + tree-only short bench lines    bench  bench.py (full: variants, isolated conv, CPU baselines)
 #   train  tools/bench_train.py   dptrain  tools/bench_train_dp.py (one nccl rank: eager DDP+SyncBN vs graphed DP step)
 #   vars   conv variants (diag lib)   modes  conv MODE ablations (tools/diag/wino3h_modes.py)
-#     lat  single-tree latency (Option A)   cycle  configs[4] on one GPU
+#   f16    the conv's f16 mode: errors, timing, headline line   lat  single-tree latency (Option A)   cycle  configs[4] on one GPU
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -63,6 +63,9 @@ for s in $STEPS; do
     vars)  timeout -k 10 400 python -u tools/diag/wino3h_variants.py ${VAR_BOARDS:-1344 2688 16384} > $OUT/variants.log 2>&1 ;;
     modes) MODES=${MODES:-0,8,1048576,1048584} timeout -k 10 300 python -u tools/diag/wino3h_modes.py ${MODE_BOARDS:-1344 16384} \
              > $OUT/modes.log 2>&1 ;;
+    f16)   timeout -k 10 300 python -u tools/diag/f16_mode_check.py > $OUT/f16_check.log 2>&1 && \
+           timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-variants --no-isolated --steps 10 --warmup 4 \
+             --evaluator fused_f16 > $OUT/quick_f16.log 2>&1 ;;
     lat)   timeout -k 10 300 python -u tools/diag/latency_single.py > $OUT/latency.log 2>&1 ;;
     cycle) timeout -k 10 900 python -u tools/bench_cycle.py --out $OUT/cycle.json ${CYCLE_ARGS:-} > $OUT/cycle.log 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

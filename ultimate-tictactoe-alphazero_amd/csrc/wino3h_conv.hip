@@ -133,7 +133,7 @@ int uttt_nn_wino3h_weights(const float *w, uint16_t *u, float *u_scale) {
 static int conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, const float *bias, const float *residual,
                           float *y, const uint32_t *x_amax, int32_t x_amax_per_board, uint32_t *y_amax,
                           uint32_t *amax_clear, int32_t clear_count, int32_t n_boards, const int32_t *n_dev,
-                          void *stream) {
+                          void *stream, bool f16 = false) {
     if (!x || !u || !bias || !y || !x_amax || n_boards < 0 || x == y || (residual && residual == y) ||
         !(u_scale > 0.0f) || clear_count < 0 || (clear_count > 0 && !amax_clear) ||
         (amax_clear && (amax_clear == y_amax || amax_clear == x_amax))) {
@@ -147,11 +147,16 @@ static int conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, cons
     if (split > 1) {
         const dim3 sgrid((unsigned)(wino3h::n_sets(n_boards > 0 ? n_boards : 1) * split));
         const hipStream_t s = (hipStream_t)stream;
-#define UTTT_WINO3S(RES, SP, R)                                                                                    \
-    hipLaunchKernelGGL((wino3h::k_wino3s_conv<RES, SP>), sgrid, dim3(64 * (8 / SP)), 0, s, x, u, u_scale, bias, R, y, \
-                       x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev)
-        if (residual) UTTT_WINO3S(true, 2, residual);
-        else UTTT_WINO3S(false, 2, nullptr);
+#define UTTT_WINO3S(RES, SP, R, M)                                                                                 \
+    hipLaunchKernelGGL((wino3h::k_wino3s_conv<RES, SP, 3, M>), sgrid, dim3(64 * (8 / SP)), 0, s, x, u, u_scale, bias, R, \
+                       y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev)
+        if (f16) {
+            if (residual) UTTT_WINO3S(true, 2, residual, wino3h::kF16);
+            else UTTT_WINO3S(false, 2, nullptr, wino3h::kF16);
+        } else {
+            if (residual) UTTT_WINO3S(true, 2, residual, 0);
+            else UTTT_WINO3S(false, 2, nullptr, 0);
+        }
 #undef UTTT_WINO3S
         hipError_t r = hipGetLastError();
         if (r != hipSuccess) {
@@ -161,12 +166,22 @@ static int conv3x3_wino3h(const float *x, const uint16_t *u, float u_scale, cons
         return UTTT_OK;
     }
     const dim3 grid(wino3h::grid_size(n_boards > 0 ? n_boards : 1));
-    if (residual)
-        hipLaunchKernelGGL(wino3h::k_wino3h_conv<true>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
-                           bias, residual, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
-    else
-        hipLaunchKernelGGL(wino3h::k_wino3h_conv<false>, grid, dim3(wino3h::NT), 0, (hipStream_t)stream, x, u, u_scale,
-                           bias, nullptr, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
+    const hipStream_t st = (hipStream_t)stream;
+    using wino3h::k_wino3h_conv;
+    if (f16) {
+        if (residual)
+            hipLaunchKernelGGL((k_wino3h_conv<true, wino3h::kF16>), grid, dim3(wino3h::NT), 0, st, x, u, u_scale, bias,
+                               residual, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
+        else
+            hipLaunchKernelGGL((k_wino3h_conv<false, wino3h::kF16>), grid, dim3(wino3h::NT), 0, st, x, u, u_scale, bias,
+                               nullptr, y, x_amax, pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
+    } else if (residual) {
+        hipLaunchKernelGGL(k_wino3h_conv<true>, grid, dim3(wino3h::NT), 0, st, x, u, u_scale, bias, residual, y, x_amax,
+                           pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
+    } else {
+        hipLaunchKernelGGL(k_wino3h_conv<false>, grid, dim3(wino3h::NT), 0, st, x, u, u_scale, bias, nullptr, y, x_amax,
+                           pb, y_amax, amax_clear, clear_count, n_boards, n_dev);
+    }
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_wino3h_conv launch: %s", hipGetErrorString(r));
@@ -192,6 +207,26 @@ int uttt_nn_conv3x3_wino3h_dev(const float *x, const uint16_t *u, float u_scale,
     }
     return conv3x3_wino3h(x, u, u_scale, bias, residual, y, x_amax, x_amax_per_board, y_amax, amax_clear, clear_count,
                           max_boards, n_dev, stream);
+}
+
+int uttt_nn_conv3x3_wino3h_f16(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                               const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                               uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, int32_t n_boards,
+                               void *stream) {
+    return conv3x3_wino3h(x, u, u_scale, bias, residual, y, x_amax, x_amax_per_board, y_amax, amax_clear, clear_count,
+                          n_boards, nullptr, stream, true);
+}
+
+int uttt_nn_conv3x3_wino3h_f16_dev(const float *x, const uint16_t *u, float u_scale, const float *bias,
+                                   const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
+                                   uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
+                                   int32_t max_boards, void *stream) {
+    if (!n_dev) {
+        set_error("uttt_nn_conv3x3_wino3h_f16_dev: n_dev required");
+        return UTTT_ERR_ARG;
+    }
+    return conv3x3_wino3h(x, u, u_scale, bias, residual, y, x_amax, x_amax_per_board, y_amax, amax_clear, clear_count,
+                          max_boards, n_dev, stream, true);
 }
 
 int uttt_nn_wino3h_set_split(int32_t split) {

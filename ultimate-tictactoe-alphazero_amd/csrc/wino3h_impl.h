@@ -62,6 +62,7 @@ constexpr int kFoldScalar = 1 << 24;    // ... as scalar v_add_f32 / v_fma_f32 p
 constexpr int kALook2 = 1 << 25;        // V fragments two points ahead (LDS latency) instead of one
 constexpr int kSerialPrologue = 1 << 26;  // sX pads zeroed and fenced before the first loads are issued
 constexpr int kSplitCvt = 1 << 27;        // f16 lo of the split by convert back, subtract, convert (round 2)
+constexpr int kF16 = (int)(1u << 31);     // f16 mode (not f32-level): M = Vhi Uhi only, U's hi plane only (uttt_nn_*_f16)
 constexpr int kL2Prefetch = 1 << 28;      // the inputs two chunks ahead touched into L2 (one dword per 128-B row)
 constexpr int kFoldAT = 1 << 18;          // the fold along u by A^T itself (rounds 1-3) instead of Z A^T
 constexpr int kEpiBarrier = 1 << 7;       // a set's epilogue starts after every wave's last point GEMMs (a barrier):
@@ -201,34 +202,42 @@ struct BFrag {
     halfx8 h, l;
 };
 constexpr int UPLANE = C * 4 * 16;  // bytes of one (xi, chunk, hi|lo) plane
+template <bool HI = false>  // HI: the hi plane only (kF16)
 __device__ __forceinline__ BFrag load_b(rsrc_t u, int xi, int chunk, int voff) {
     const int soff = (xi * NCH + chunk) * 2 * UPLANE;
     BFrag b;
     b.h = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff, soff, 0));
-    b.l = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff + UPLANE, soff, 0));
+    if constexpr (HI) b.l = b.h;
+    else b.l = __builtin_bit_cast(halfx8, __builtin_amdgcn_raw_buffer_load_b128(u, voff + UPLANE, soff, 0));
     return b;
 }
 // the XI-th point a wave visits: the points in order from ROT (0 in the product)
 template <int XI, int ROT>
 __host__ __device__ constexpr int pt() { return (XI + ROT) % NP; }
-template <int XI, int ROT = 0>
+template <int XI, int ROT = 0, bool HI = false>
 __device__ __forceinline__ BFrag load_b_ahead(rsrc_t u, int chunk, int voff) {
-    if constexpr (XI < NP) return load_b(u, pt<XI, ROT>(), chunk, voff);
-    else return load_b(u, pt<XI - NP, ROT>(), (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
+    if constexpr (XI < NP) return load_b<HI>(u, pt<XI, ROT>(), chunk, voff);
+    else return load_b<HI>(u, pt<XI - NP, ROT>(), (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
 }
 
 // A fragments (V hi / lo of both row blocks) of one point
 struct AFrag {
     halfx8 h0, l0, h1, l1;
 };
+template <bool HI = false>  // HI: the hi planes only (kF16)
 __device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
     // sv already points at this lane's 16-byte slot within a plane
     const char *p = sv + xi * 4 * VPLANE;
     AFrag a;
     a.h0 = *reinterpret_cast<const halfx8 *>(p);
-    a.l0 = *reinterpret_cast<const halfx8 *>(p + VPLANE);
     a.h1 = *reinterpret_cast<const halfx8 *>(p + 2 * VPLANE);
-    a.l1 = *reinterpret_cast<const halfx8 *>(p + 3 * VPLANE);
+    if constexpr (HI) {
+        a.l0 = a.h0;
+        a.l1 = a.h1;
+    } else {
+        a.l0 = *reinterpret_cast<const halfx8 *>(p + VPLANE);
+        a.l1 = *reinterpret_cast<const halfx8 *>(p + 3 * VPLANE);
+    }
     return a;
 }
 
@@ -246,20 +255,20 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
                 b2 = bq[0];
                 asm volatile("" : "+v"(b2.h), "+v"(b2.l));
             } else {
-                b2 = load_b_ahead<XI + PF, ROT>(u, chunk, voff);
+                b2 = load_b_ahead<XI + PF, ROT, (MODE & kF16) != 0>(u, chunk, voff);
             }
             const BFrag b0 = bq[0];
-            if constexpr (MODE & kNoALookahead) a0 = load_a(sv, pt<XI, ROT>());  // this point's V, waited for here
+            if constexpr (MODE & kNoALookahead) a0 = load_a<(MODE & kF16) != 0>(sv, pt<XI, ROT>());  // this point's V, waited for here
             AFrag a1, a2;
             if constexpr (MODE & kALook2) {  // a_next holds point XI+1 (loaded a point ago); load XI+2
                 if constexpr (XI + 1 < NP) a1 = *a_next;
-                if constexpr (XI + 2 < NP) a2 = load_a(sv, pt<XI + 2, ROT>());
+                if constexpr (XI + 2 < NP) a2 = load_a<(MODE & kF16) != 0>(sv, pt<XI + 2, ROT>());
             } else if constexpr (XI + 1 < NP && !(MODE & kNoALookahead)) {
                 if constexpr (MODE & 16) {  // diagnostic: no A loads
                     a1 = a0;
                     asm volatile("" : "+v"(a1.h0), "+v"(a1.l0), "+v"(a1.h1), "+v"(a1.l1));
                 } else {
-                    a1 = load_a(sv, pt<XI + 1, ROT>());
+                    a1 = load_a<(MODE & kF16) != 0>(sv, pt<XI + 1, ROT>());
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -271,19 +280,34 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
                 m1 = floatx4{S[srow].p[2].x, S[srow].p[2].y, S[srow].p[3].x, S[srow].p[3].y};
             }
             constexpr bool fold_here = XI > 0 && !(MODE & 64);
-            // small terms first, then the hi x hi product
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h0, m0, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 0, MODE>(S, mprev, k2, k4);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h1, m1, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 1, MODE>(S, mprev, k2, k4);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l0, m0, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 2, MODE>(S, mprev, k2, k4);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l1, m1, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 3, MODE>(S, mprev, k2, k4);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h0, m0, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 4, MODE>(S, mprev, k2, k4);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
-            if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 5, MODE>(S, mprev, k2, k4);
+            if constexpr (MODE & kF16) {  // the hi x hi product alone, the fold spread over its two MFMAs
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h0, m0, 0, 0, 0);
+                if constexpr (fold_here) {
+                    fold_slot<pt<XI - 1, ROT>(), 0, MODE>(S, mprev, k2, k4);
+                    fold_slot<pt<XI - 1, ROT>(), 1, MODE>(S, mprev, k2, k4);
+                    fold_slot<pt<XI - 1, ROT>(), 2, MODE>(S, mprev, k2, k4);
+                }
+                m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
+                if constexpr (fold_here) {
+                    fold_slot<pt<XI - 1, ROT>(), 3, MODE>(S, mprev, k2, k4);
+                    fold_slot<pt<XI - 1, ROT>(), 4, MODE>(S, mprev, k2, k4);
+                    fold_slot<pt<XI - 1, ROT>(), 5, MODE>(S, mprev, k2, k4);
+                }
+            } else {
+                // small terms first, then the hi x hi product
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h0, m0, 0, 0, 0);
+                if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 0, MODE>(S, mprev, k2, k4);
+                m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.l, a0.h1, m1, 0, 0, 0);
+                if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 1, MODE>(S, mprev, k2, k4);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l0, m0, 0, 0, 0);
+                if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 2, MODE>(S, mprev, k2, k4);
+                m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.l1, m1, 0, 0, 0);
+                if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 3, MODE>(S, mprev, k2, k4);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h0, m0, 0, 0, 0);
+                if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 4, MODE>(S, mprev, k2, k4);
+                m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0.h, a0.h1, m1, 0, 0, 0);
+                if constexpr (fold_here) fold_slot<pt<XI - 1, ROT>(), 5, MODE>(S, mprev, k2, k4);
+            }
             asm volatile("" : "+v"(m0), "+v"(m1));  // keep this point's MFMAs in its own region
             if constexpr (acc_direct<P, MODE>()) {
                 S[srow].p[0] = __builtin_shufflevector(m0, m0, 0, 1);
@@ -441,7 +465,7 @@ __device__ __forceinline__ void transform_rows(floatx2 (&uu)[5][5], const float 
     }
 }
 
-template <bool MIX = true>
+template <bool MIX = true, bool HI = false>
 __device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floatx2 (&uu)[5][5], int it) {
     const int p = it % (KC / 2), lt = it / (KC / 2);
     // A fragment: lane (row m, kq) holds k = 8kq..8kq+7; channel pair p is k = 2p, 2p+1
@@ -458,16 +482,16 @@ __device__ __forceinline__ void transform_cols(char *__restrict__ sv, const floa
             split<MIX>(o[a], hi, lo);
             char *q = base + (a * 5 + b) * 4 * VPLANE;
             *reinterpret_cast<uint32_t *>(q) = hi;
-            *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;
+            if constexpr (!HI) *reinterpret_cast<uint32_t *>(q + VPLANE) = lo;  // kF16 never reads lo
         }
     }
 }
 
-template <bool MIX = true>
+template <bool MIX = true, bool HI = false>
 __device__ __forceinline__ void transform(char *__restrict__ sv, const float *__restrict__ sX, int it, int h) {
     floatx2 uu[5][5];
     transform_rows(uu, sX, it, h);
-    transform_cols<MIX>(sv, uu, it);
+    transform_cols<MIX, HI>(sv, uu, it);
 }
 
 // An opaque copy: index math derived from it is recomputed where it is used
@@ -806,7 +830,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
     const int rot = ((MODE & kStagger) && wv >= 4) ? kStaggerRot : 0;
     BFrag bq[PF];
 #pragma unroll
-    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, (i + rot) % NP, c_rot, voff);
+    for (int i = 0; i < PF; ++i) bq[i] = load_b<(MODE & kF16) != 0>(ur, (i + rot) % NP, c_rot, voff);
     if constexpr (!(MODE & kSerialPrologue)) zero_pads();
     store_x(sX, xr, sc, tid);
     __syncthreads();
@@ -838,7 +862,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         SetScale sc_next = sc;
         if (c == NCH - 1 && g + 1 < G) sc_next = set_scale(x_amax, x_amax_per_board, set_b0(g + 1), n_boards);
         mark(g, 0, t0);
-        if constexpr ((MODE & 3) != 1) transform<!(MODE & kSplitCvt)>(sV, sX, fresh(tid), set_of(g) & 1);
+        if constexpr ((MODE & 3) != 1) transform<!(MODE & kSplitCvt), (MODE & kF16) != 0>(sV, sX, fresh(tid), set_of(g) & 1);
         mark(g, 1, t0);
         lds_barrier();
         if (g + 1 < G) store_x(sX, xr, sc_next, fresh(tid));
@@ -847,8 +871,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             if (c == NCH - 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
         if constexpr ((MODE & 3) != 2) {
             AFrag a0, an;
-            if constexpr (!(MODE & kNoALookahead)) a0 = load_a(sv_lane, rot);
-            if constexpr (MODE & kALook2) an = load_a(sv_lane, (1 + rot) % NP);
+            if constexpr (!(MODE & kNoALookahead)) a0 = load_a<(MODE & kF16) != 0>(sv_lane, rot);
+            if constexpr (MODE & kALook2) an = load_a<(MODE & kF16) != 0>(sv_lane, (1 + rot) % NP);
             floatx2 mprev[4];
             if ((MODE & kStagger) && rot) xi_loop<0, MODE, PF, kStaggerRot>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
             else xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
@@ -881,7 +905,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
 // synchronous and covers the boards in the batch only; the transform covers only the tile slots
 // that hold a tile of such a board (the others' V columns are stale, their MFMA columns independent,
 // their results dropped by the epilogue).
-template <bool RES, int SPLIT, int PF = 3>
+template <bool RES, int SPLIT, int PF = 3, int MODE = 0>
 __global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *__restrict__ x,
                                                                  const uint16_t *__restrict__ u, float u_scale,
                                                                  const float *__restrict__ bias,
@@ -922,7 +946,7 @@ __global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *_
     const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (2 * kq)) * 16);
     BFrag bq[PF];
 #pragma unroll
-    for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, 0, voff);
+    for (int i = 0; i < PF; ++i) bq[i] = load_b<(MODE & kF16) != 0>(ur, i, 0, voff);
     const SetScale sc = set_scale(x_amax, x_amax_per_board, b0, n_boards);
     for (int i = tid; i < NPAD * (KC / 4); i += NTS) {  // the zero pads of the staged layout (as the product)
         const int j = i / (KC / 4), q = i % (KC / 4);
@@ -942,11 +966,11 @@ __global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *_
             reinterpret_cast<float4 *>(sX + sp * KC)[q] = make_float4(t.x * sv, t.y * sv, t.z * sv, t.w * sv);
         }
         lds_barrier();
-        for (int it = tid; it < live_slots * (KC / 2); it += NTS) transform(sV, sX, it, h);
+        for (int it = tid; it < live_slots * (KC / 2); it += NTS) transform<true, (MODE & kF16) != 0>(sV, sX, it, h);
         lds_barrier();
-        AFrag a0 = load_a(sv_lane, 0), an;
+        AFrag a0 = load_a<(MODE & kF16) != 0>(sv_lane, 0), an;
         floatx2 mprev[4];
-        xi_loop<0, 0, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
+        xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
         lds_barrier();  // sX and sV are rewritten by the next chunk
     }
     set_epilogue<RES, 0>(S, st, sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, wave_base, s_bmax);

@@ -99,16 +99,24 @@ class FusedNetworkEvaluator:
     """Leaf evaluator over an engine's pending leaves (needs_input = False: the stem reads
     the leaves' bitboards, the engine never builds the NCHW tensor). device_count: called
     with a RoundCount (after Engine.select_async) it reads the leaf count on the device, so
-    the round needs no host synchronisation."""
+    the round needs no host synchronisation.
+
+    precision: "f32" (default; the split-f16 tower, within 1e-5 of the fp32 DualNetwork) or "f16"
+    (uttt_nn_conv3x3_wino3h_f16: one f16 product per point, ~1e-3 relative: the optional fast
+    evaluator, not the reference's numerics); None reads UTTT_NN_PRECISION (default f32)."""
     needs_input = False
     device_count = True
     NROW = 4  # per-board max rows, rotated over the 32 convs (see __init__, _tower_heads)
 
-    def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None):
+    def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None, precision=None):
+        import os
         net = net.eval()
         if conv != "wino3h":
             raise ValueError("conv must be 'wino3h' (the split-f16 Winograd tower; the f32-MFMA kernel was retired)")
         self.conv = conv
+        self.precision = precision or os.environ.get("UTTT_NN_PRECISION", "f32")
+        if self.precision not in ("f32", "f16"):
+            raise ValueError("precision must be 'f32' (split-f16, f32-level) or 'f16' (one f16 product)")
         self.engine = engine
         self.lib = _lib.load()
         if engine is not None:
@@ -204,7 +212,8 @@ class FusedNetworkEvaluator:
             if self.tower_events is not None:
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ev0.record()
-            fn = self.lib.uttt_nn_conv3x3_wino3h_dev
+            fn = self.lib.uttt_nn_conv3x3_wino3h_f16_dev if self.precision == "f16" else \
+                self.lib.uttt_nn_conv3x3_wino3h_dev
             for a in calls:
                 check(fn(*a))
             if self.tower_events is not None:
@@ -218,7 +227,7 @@ class FusedNetworkEvaluator:
             ev0.record()
         rows = [ctypes.c_void_p(self.bamax[r].data_ptr()) for r in range(self.NROW)]
         cap = self.max_batch
-        fn = self.lib.uttt_nn_conv3x3_wino3h
+        fn = self.lib.uttt_nn_conv3x3_wino3h_f16 if self.precision == "f16" else self.lib.uttt_nn_conv3x3_wino3h
         i = 0
         for (u1, s1, b1), (u2, s2, b2) in self.wino:
             src = (_p(self.stem_amax), 0) if i == 0 else (rows[(i - 1) % 4], 1)
@@ -273,16 +282,18 @@ def board_amax(x):
     return x.abs().reshape(x.shape[0], -1).amax(dim=1).contiguous().view(torch.int32)
 
 
-def conv3x3_wino3h(x, u, su, bias, residual=None, y_amax=None, x_amax=None):
+def conv3x3_wino3h(x, u, su, bias, residual=None, y_amax=None, x_amax=None, precision="f32"):
     """Test/utility wrapper for the split-f16 F(3x3,3x3) kernel: x (n,81,128) f32 cuda ->
     relu(conv3x3(x) + bias (+ residual)); u, su from wino3h_weights(). x_amax: per-board
-    max rows (default: computed from x); y_amax: optional (n,) int32 row receiving max(y) per board."""
+    max rows (default: computed from x); y_amax: optional (n,) int32 row receiving max(y) per board.
+    precision "f16": the one-product f16 mode (uttt_nn_conv3x3_wino3h_f16)."""
     y = torch.empty_like(x)
     xa = board_amax(x) if x_amax is None else x_amax
-    check(_lib.load().uttt_nn_conv3x3_wino3h(_p(x), _p(u), ctypes.c_float(su), _p(bias),
-                                             _p(residual) if residual is not None else None, _p(y), _p(xa), 1,
-                                             _p(y_amax) if y_amax is not None else None, None, 0, x.shape[0],
-                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    lib = _lib.load()
+    fn = lib.uttt_nn_conv3x3_wino3h_f16 if precision == "f16" else lib.uttt_nn_conv3x3_wino3h
+    check(fn(_p(x), _p(u), ctypes.c_float(su), _p(bias), _p(residual) if residual is not None else None, _p(y), _p(xa),
+             1, _p(y_amax) if y_amax is not None else None, None, 0, x.shape[0],
+             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     return y
 
 
