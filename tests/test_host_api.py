@@ -207,3 +207,30 @@ def test_winograd3_algebra_matches_direct_conv(engine_lib):
         for kx in range(3):
             direct += np.einsum("rsc,oc->rso", xp[ky:ky + 9, kx:kx + 9], w[:, :, ky, kx].astype(np.float64))
     assert np.abs(y - direct).max() < 1e-5 * np.abs(direct).max()
+
+
+def test_main_board_line_check_is_the_reference_eight_compares(uttt_cpp_mod):
+    """win9 (uttt_bits.h) is written as shifted ANDs for the rows and columns (round 5); is_lose reads it on the
+    opponent's main board (uttt_game.cpp:77-79), so every one of the 512 masks there must give the reference's
+    eight-line check (uttt_game.cpp:35-61), and next() must find a small-board win for every cell of every
+    board shape (it runs win9 on the board just played, with the small-range divisions by 9 and 27)."""
+    m = uttt_cpp_mod
+    lines = (0x007, 0x038, 0x1C0, 0x049, 0x092, 0x124, 0x111, 0x054)
+    empty = [[0] * 9 for _ in range(9)]
+    for mask in range(512):
+        main_e = [(mask >> i) & 1 for i in range(9)]
+        s = m.State(empty, empty, [0] * 9, main_e, -1)
+        assert s.is_lose() == any((mask & x) == x for x in lines), mask
+    # the mover completes a line on small board b by playing cell c: the board is won in the next state
+    for b in range(9):
+        for line in lines:
+            for c in range(9):
+                if not (line >> c) & 1:
+                    continue
+                own = [row[:] for row in empty]
+                for i in range(9):
+                    if (line >> i) & 1 and i != c:
+                        own[b][i] = 1
+                s = m.State(own, empty, [0] * 9, [0] * 9, b)
+                nx = s.next(9 * b + c)
+                assert nx.main_board_enemy_pieces[b] == 1, (b, line, c)

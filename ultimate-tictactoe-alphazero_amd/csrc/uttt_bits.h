@@ -29,16 +29,24 @@ constexpr uint64_t kGold = 0x9E3779B97F4A7C15ull;
 
 UTTT_HD uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 
-// 3-in-a-row on a 9-bit board (uttt_game.cpp:35-61: rows, columns, diagonals).
+// Division of small non-negative ints by 9, 27 and 3 as one 24-bit multiply and a shift: exact for
+// 0..511 (tests/test_host_api.py checks every value); the general forms are 32-bit mul_hi sequences,
+// a quarter-rate instruction each, on the descent's critical path.
+UTTT_HD int div9(int a) { return (a * 57) >> 9; }
+UTTT_HD int div27(int a) { return (a * 19) >> 9; }
+UTTT_HD int div3(int a) { return (a * 171) >> 9; }
+
+// 3-in-a-row on a 9-bit board (uttt_game.cpp:35-61: rows, columns, diagonals): a row is full when
+// bits i, i+1, i+2 are (i = 0, 3, 6), a column when i, i+3, i+6 are (i = 0, 1, 2); the diagonals 0x111,
+// 0x054 by compares. Equal to the eight compares of the reference for all 512 masks (tests).
 UTTT_HD bool win9(uint32_t m) {
-    return ((m & 0x007u) == 0x007u) | ((m & 0x038u) == 0x038u) | ((m & 0x1C0u) == 0x1C0u) |
-           ((m & 0x049u) == 0x049u) | ((m & 0x092u) == 0x092u) | ((m & 0x124u) == 0x124u) |
-           ((m & 0x111u) == 0x111u) | ((m & 0x054u) == 0x054u);
+    return ((m & (m >> 1) & (m >> 2) & 0x049u) | (m & (m >> 3) & (m >> 6) & 0x007u)) != 0u ||
+           (m & 0x111u) == 0x111u || (m & 0x054u) == 0x054u;
 }
 
 UTTT_HD uint32_t main_own(const uttt_state_t &s) { return s.mains & kCells; }
 UTTT_HD uint32_t main_opp(const uttt_state_t &s) { return (s.mains >> 16) & kCells; }
-UTTT_HD uint32_t cells_of(uint32_t word, int b) { return (word >> (9 * (b % 3))) & kCells; }
+UTTT_HD uint32_t cells_of(uint32_t word, int b) { return (word >> (9 * (b - 3 * div3(b)))) & kCells; }
 
 UTTT_HD bool is_lose(const uttt_state_t &s) { return win9(main_opp(s)); }
 
@@ -82,7 +90,7 @@ UTTT_HD bool is_first_player(const uttt_state_t &s) {  // uttt_game.cpp:92-94
 // the new opponent set; a won small board sets the new opponent's main bit, a
 // full one sets both; the next active board is the cell unless it is closed.
 UTTT_HD uttt_state_t next_state(const uttt_state_t &s, int a) {
-    const int b = a / 9, c = a % 9, w = a / 27;
+    const int b = div9(a), c = a - 9 * b, w = div27(a);
     uttt_state_t n;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -92,7 +100,7 @@ UTTT_HD uttt_state_t next_state(const uttt_state_t &s, int a) {
     uint32_t mown = main_opp(s), mopp = main_own(s);
     // word w chosen by selects, not a dynamic index into the local arrays (which the device
     // compiler may place in scratch)
-    const uint32_t bit = 1u << (a % 27);
+    const uint32_t bit = 1u << (a - 27 * w);
     n.opp[0] |= w == 0 ? bit : 0u;
     n.opp[1] |= w == 1 ? bit : 0u;
     n.opp[2] |= w == 2 ? bit : 0u;
@@ -122,9 +130,9 @@ UTTT_HD int action_at(int pos) {
 }
 // the word chosen by selects, not a dynamic index (which puts a local state in LDS or scratch)
 UTTT_HD uint32_t bit_of(const uint32_t w[3], int a) {
-    const int i = a / 27;
+    const int i = div27(a);
     const uint32_t x = i == 0 ? w[0] : (i == 1 ? w[1] : w[2]);
-    return (x >> (a % 27)) & 1u;
+    return (x >> (a - 27 * i)) & 1u;
 }
 
 // ---------------------------------------------------------------------------
