@@ -29,7 +29,7 @@ constexpr int C = 128;  // DN_FILTERS
 // per (leaf, output position) the 27-bit mask of set input taps; then each thread
 // sums the weight rows of the set taps for (leaf, position, 4 channels) items and
 // stores float4s (a wave covers two positions: little divergence in the tap loop).
-constexpr int SB = 4;
+constexpr int SB = 2;  // round 5: 4 -> 2 (a 1,370-leaf launch is 685 workgroups, at most 6 leaves per CU instead of 8)
 __device__ __forceinline__ uint32_t bit3(uint32_t w0, uint32_t w1, uint32_t w2, int a) {
     // bit a of a 81-bit board held in three 27-bit words, without indexing an array
     // (a dynamically indexed local array lands in scratch memory)
@@ -46,7 +46,16 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
     if (s0 >= n) return;
     const int nb = n - s0 < SB ? n - s0 : SB;
     const int t = threadIdx.x;
-    for (int i = t; i < 27 * (C / 4); i += 256) s_w[i] = reinterpret_cast<const float4 *>(w)[i];
+    {
+        constexpr int NW_ = (27 * (C / 4) + 255) / 256;  // weight rows: every load in flight before the stores
+        float4 wr[NW_];
+#pragma unroll
+        for (int k = 0; k < NW_; ++k)
+            if (t + 256 * k < 27 * (C / 4)) wr[k] = reinterpret_cast<const float4 *>(w)[t + 256 * k];
+#pragma unroll
+        for (int k = 0; k < NW_; ++k)
+            if (t + 256 * k < 27 * (C / 4)) s_w[t + 256 * k] = wr[k];
+    }
     for (int i = t; i < nb * 81; i += 256) {
         const uttt_state_t s = leaf[tree_of ? tree_of[s0 + i / 81] : s0 + i / 81];
         uint32_t lm[3];
