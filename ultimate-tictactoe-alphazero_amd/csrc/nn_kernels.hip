@@ -46,16 +46,7 @@ __global__ __launch_bounds__(256) void k_stem(const uttt_state_t *__restrict__ l
     if (s0 >= n) return;
     const int nb = n - s0 < SB ? n - s0 : SB;
     const int t = threadIdx.x;
-    {
-        constexpr int NW_ = (27 * (C / 4) + 255) / 256;  // weight rows: every load in flight before the stores
-        float4 wr[NW_];
-#pragma unroll
-        for (int k = 0; k < NW_; ++k)
-            if (t + 256 * k < 27 * (C / 4)) wr[k] = reinterpret_cast<const float4 *>(w)[t + 256 * k];
-#pragma unroll
-        for (int k = 0; k < NW_; ++k)
-            if (t + 256 * k < 27 * (C / 4)) s_w[t + 256 * k] = wr[k];
-    }
+    for (int i = t; i < 27 * (C / 4); i += 256) s_w[i] = reinterpret_cast<const float4 *>(w)[i];
     for (int i = t; i < nb * 81; i += 256) {
         const uttt_state_t s = leaf[tree_of ? tree_of[s0 + i / 81] : s0 + i / 81];
         uint32_t lm[3];
