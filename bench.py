@@ -498,6 +498,32 @@ def hbm_roofline(name, stat, trees_per_launch, pmc_name=None, evaluator=None, si
             "event_avg_launch_us": round(ev_us, 2), "launches": stat["launches"]}
 
 
+def fused_rounds(evaluator):
+    """Hash-evaluator rounds run the previous round's apply and this round's select as one k_round launch
+    (uttt_round_hash_async; UTTT_FUSED_ROUNDS=0 keeps k_select and k_apply apart)."""
+    return evaluator == "hash" and os.environ.get("UTTT_FUSED_ROUNDS", "1") != "0"
+
+
+def tree_rooflines(stats, trees, evaluator, sims, pmc_sel, pmc_app):
+    """(select roofline, backup roofline) of the tree kernels. Fused rounds: one roofline for k_round, whose
+    launches carry both kernels' algorithmic bytes (the first round of a move is a plain k_select and the
+    move's last staged apply a plain k_apply; their launches are included, a move's 1 of ~9)."""
+    sel, app = stats["select"], stats["apply"]
+    if not fused_rounds(evaluator):
+        return (hbm_roofline("k_select (PUCT descent, one wave per tree)", sel, trees, pmc_sel, evaluator, sims),
+                hbm_roofline("k_apply (expand + backup, one wave per pending leaf)", app, trees, pmc_app, evaluator,
+                             sims))
+    merged = {"ms": sel["ms"] + app["ms"], "launches": sel["launches"] + app["launches"],
+              "bytes": sel["bytes"] + app["bytes"]}
+    rf = hbm_roofline("k_round (the previous round's expand + backup, then this round's PUCT descent; one wave "
+                      "per tree)", merged, trees, "pmc_round_tree.json" if pmc_sel else None, evaluator, sims)
+    rf["fused"] = {"select_bytes": sel["bytes"], "apply_bytes": app["bytes"], "k_select_or_round_launches":
+                   sel["launches"], "k_apply_launches": app["launches"]}
+    return rf, {"kernel": "k_apply", "fused_into": "k_round", "algo_bytes_per_round": round(app["bytes"] / max(
+        sel["launches"], 1)), "note": "hash-evaluator rounds apply inside k_round (roofline_select); "
+                                      "UTTT_FUSED_ROUNDS=0 measures k_apply on its own"}
+
+
 def main():
     args = parse()
     if args.cpu_baseline_child:
@@ -578,12 +604,10 @@ def main():
                               "(cache off) is the configs[1] measurement")
             if cfg["evaluator"] == "hash":
                 sv["net"] = None
-                sv["roofline_select"] = hbm_roofline("k_select", rv["stats"]["select"], rv["trees_per_launch"],
-                                                     "pmc_select_tree.json" if cfg["sims"] == S else None,
-                                                     "hash", cfg["sims"])
-                sv["roofline_backup"] = hbm_roofline("k_apply", rv["stats"]["apply"], rv["trees_per_launch"],
-                                                     "pmc_apply_tree.json" if cfg["sims"] == S else None,
-                                                     "hash", cfg["sims"])
+                sv["roofline_select"], sv["roofline_backup"] = tree_rooflines(
+                    rv["stats"], rv["trees_per_launch"], "hash", cfg["sims"],
+                    "pmc_select_tree.json" if cfg["sims"] == S else None,
+                    "pmc_apply_tree.json" if cfg["sims"] == S else None)
                 sv["breakdown_ms"] = {k: round(rv["stats"][k]["ms"], 2) for k in ("select", "apply", "scan", "move_end")}
                 sv["breakdown_ms"]["evaluator"] = round(rv["nn_ms"], 2)
                 sv["breakdown_ms"]["wall"] = round(rv["elapsed"] * 1e3, 2)
@@ -619,6 +643,7 @@ def main():
         tree = args.evaluator == "hash"
         pmc_sel = "pmc_select_tree.json" if tree else "pmc_select.json"
         pmc_app = "pmc_apply_tree.json" if tree else "pmc_apply.json"
+        tree_rf = tree_rooflines(st, r["trees_per_launch"], args.evaluator, S, pmc_sel, pmc_app)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -656,10 +681,8 @@ def main():
                 "parallelism": f"games sharded over {world} GPU(s) by contiguous global-id blocks, "
                                f"no data-path collective",
             },
-            "roofline": conv_roofline(r, args.steps) if conv else hbm_roofline("k_select", sel, r["trees_per_launch"],
-                                                                   pmc_sel, args.evaluator, S),
-            "roofline_select": dict(hbm_roofline("k_select (PUCT descent, one wave per tree)", sel,
-                                                 r["trees_per_launch"], pmc_sel, args.evaluator, S),
+            "roofline": conv_roofline(r, args.steps) if conv else tree_rf[0],
+            "roofline_select": dict(tree_rf[0],
                                     latency_model={
                                         "levels_per_tree_per_launch": round(st["select_levels"]["bytes"] / lev_trees, 2),
                                         "slowest_tree_levels_per_launch": round(max_lev, 1),
@@ -676,8 +699,7 @@ def main():
                                                 "payload, re-check, path update and fence); predicted = that chain x "
                                                 "the dependent-load latency of tools/diag/chase.hip (2,048 waves, "
                                                 "random 256-B loads that miss L2)"}),
-            "roofline_backup": hbm_roofline("k_apply (expand + backup, one wave per pending leaf)", st["apply"],
-                                            r["trees_per_launch"], pmc_app, args.evaluator, S),
+            "roofline_backup": tree_rf[1],
             "nn": {"rows_evaluated": r["rows"], "ms": round(r["nn_ms"], 2),
                    "share_of_step": round(r["nn_ms"] / 1e3 / r["elapsed"], 4),
                    "lane_sum_ms": round(r["nn_lane_sum_ms"], 2),

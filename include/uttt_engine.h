@@ -190,11 +190,15 @@ int uttt_eval_hash_dev(uttt_engine_t *eng, float *policy, float *value);
 /* One whole round with the hash evaluator, enqueued by one call (round 5; the rounds of
  * SelfPlay.steps with HashEvaluator lanes, i.e. the kernel microbenchmark of SURVEY §8(d)):
  * uttt_search_select_async_to(ring_slot) -> uttt_eval_hash_dev(policy, value) ->
- * uttt_search_apply(on_device). The scan stores the round's counts and then `tag` (word 3 of the
- * slot, a system-scope release store), so the host learns that the counts landed by polling the
- * tag: no event and no host sync per round. policy: (max_trees, 81) f32, value: (max_trees,) f32,
- * device memory. Replaces, for the test evaluator, one pass of the flush loop of
- * uttt_mcts.cpp:109-167 over every tree. */
+ * uttt_search_apply(on_device), with the apply staged: the next call runs it and its own select as
+ * one launch (k_round: per tree, the previous evaluation applied, then the next descent), and any
+ * other call that reads the trees (the move's end, the root results, a synchronous select) applies
+ * it first. UTTT_FUSED_ROUNDS=0 launches the three steps as written above. The scan stores the
+ * round's counts and then `tag` (word 3 of the slot, a system-scope release store), so the host
+ * learns that the counts landed by polling the tag: no event and no host sync per round. policy:
+ * (max_trees, 81) f32, value: (max_trees,) f32, device memory, left untouched until the staged apply
+ * has run. Replaces, for the test evaluator, one pass of the flush loop of uttt_mcts.cpp:109-167
+ * over every tree. */
 int uttt_round_hash_async(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, float *policy, float *value);
 
 /* Root results after the search: visit counts of the root's children (legal

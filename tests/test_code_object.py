@@ -26,6 +26,7 @@ PRODUCT = {
     "k_finalize": "10k_finalizeE",
     "k_archive": "9k_archiveE",
     "k_flush1<cpp>": "8k_flush1ILb0E",
+    "k_round<cpp>": "7k_roundILb0E",
     "k_stem": "6k_stemE",
     "k_heads": "7k_headsE",
 }

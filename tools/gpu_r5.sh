@@ -6,7 +6,7 @@
 #   fcal   FETCH_SIZE calibration on k_select's load shapes (tools/diag/fetch_cal under two rocprofv3 --pmc passes)
 #   tprof  tree-only bench (hash evaluator, one lane) under rocprofv3 --kernel-trace --stats + prof_summary
 #   hprof  the headline bench under rocprofv3 --kernel-trace --stats + prof_summary
-#   pmcsel / pmctree  k_select / k_apply PMC traffic (headline / tree-only population)
+#   pmcsel / pmctree  k_select / k_apply PMC traffic (headline / tree-only population, unfused)   pmcround  k_round (fused)
 #   quick  headline + tree-only short bench lines    bench  bench.py (full: variants, isolated conv, CPU baselines)
 #   train  tools/bench_train.py   dptrain  tools/bench_train_dp.py (one nccl rank: eager DDP+SyncBN vs graphed DP step)
 #   vars   conv variants (diag lib)   modes  conv MODE ablations (tools/diag/wino3h_modes.py)
@@ -43,11 +43,15 @@ for s in $STEPS; do
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/hprof_bench.log 2>&1 && \
            python3 tools/prof_summary.py $(ls $OUT/hprof/*/bench_kernel_trace.csv $OUT/hprof/bench_kernel_trace.csv 2>/dev/null | head -1) \
                $OUT/hprof_bench.log $OUT/prof_headline.md > $OUT/hprof_summary.log 2>&1 ;;
-    pmctree) PMC_OUT=$OUT/pmc_tree PMC_AGE=100 PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
+    pmctree) UTTT_FUSED_ROUNDS=0 PMC_OUT=$OUT/pmc_tree PMC_AGE=100 PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
                > $OUT/pmc_tree.log 2>&1 && \
              python tools/pmc_summary.py $OUT/pmc_tree $OUT/pmc_tree/p1.log $OUT/pmc_select_tree.json k_select >> $OUT/pmc_tree.log && \
              python tools/pmc_summary.py $OUT/pmc_tree $OUT/pmc_tree/p1.log $OUT/pmc_apply_tree.json k_apply >> $OUT/pmc_tree.log && \
              rm -rf $OUT/pmc_tree/p1 $OUT/pmc_tree/p2 $OUT/pmc_tree/p3 ;;
+    pmcround) PMC_OUT=$OUT/pmc_round PMC_AGE=100 PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
+               > $OUT/pmc_round.log 2>&1 && \
+             python tools/pmc_summary.py $OUT/pmc_round $OUT/pmc_round/p1.log $OUT/pmc_round_tree.json k_round >> $OUT/pmc_round.log && \
+             rm -rf $OUT/pmc_round/p1 $OUT/pmc_round/p2 $OUT/pmc_round/p3 ;;
     pmcsel) PMC_OUT=$OUT/pmc_sel timeout -k 10 900 bash tools/pmc_select.sh > $OUT/pmc_select.log 2>&1 && \
              python tools/pmc_summary.py $OUT/pmc_sel $OUT/pmc_sel/p1.log $OUT/pmc_select.json k_select >> $OUT/pmc_select.log && \
              python tools/pmc_summary.py $OUT/pmc_sel $OUT/pmc_sel/p1.log $OUT/pmc_apply.json k_apply >> $OUT/pmc_select.log && \

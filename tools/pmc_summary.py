@@ -7,7 +7,7 @@ FETCH_SIZE counts 64 B per 128-B read request (MI355X_MICROARCH.md, HBM), i.e.
 it can under-report wide coalesced reads by 2x; k_select's reads are 4 B/lane
 and uncalibrated, so both the raw and the doubled read figure are kept.
 
-usage: pmc_summary.py PMC_DIR BENCH_LOG OUT.json [KERNEL]   (k_select default, or k_apply)
+usage: pmc_summary.py PMC_DIR BENCH_LOG OUT.json [KERNEL]   (k_select default, k_apply, or k_round)
 """
 import csv
 import json
@@ -26,7 +26,8 @@ def main(d, bench_log, out, kernel="k_select"):
     write, nw = per_launch(f"{d}/p2/t_counter_collection.csv", "WRITE_SIZE", kernel)
     rdreq, _ = per_launch(f"{d}/p3/t_counter_collection.csv", "TCC_EA0_RDREQ_sum", kernel)
     bench = json.loads([ln for ln in open(bench_log).read().splitlines() if ln.startswith("{")][-1])
-    roof = bench["roofline_select"] if kernel == "k_select" else bench["roofline_backup"]
+    # k_round (fused hash rounds): the select roofline carries both kernels' algorithmic bytes
+    roof = bench["roofline_select"] if kernel in ("k_select", "k_round") else bench["roofline_backup"]
     res = {
         "kernel": kernel,
         "launches_averaged": [nf, nw],

@@ -28,8 +28,10 @@ def main(trace, bench_log, out):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                          int(r["VGPR_Count"]), int(r["SGPR_Count"]), int(r["Scratch_Size"])))
     rows.sort()
-    sel = [r for r in rows if "k_select" in r[2]]
     rs = bench.get("roofline_select", bench["roofline"])
+    # fused hash rounds: the select roofline's launches are k_round, k_select (first rounds) and k_apply (flushes)
+    names = ("k_round", "k_select", "k_apply") if rs["kernel"].startswith("k_round") else ("k_select",)
+    sel = [r for r in rows if any(n in r[2] for n in names)]
     nwin = rs["launches"]
     t0 = sel[-nwin][0] if len(sel) >= nwin else rows[0][0]
     win = [r for r in rows if r[0] >= t0]
@@ -52,7 +54,7 @@ def main(trace, bench_log, out):
     seen = set()
     for key in ("roofline", "roofline_select", "roofline_backup"):
         rf = bench.get(key)
-        if not rf or rf["kernel"].split()[0] in seen:
+        if not rf or "unit" not in rf or rf["kernel"].split()[0] in seen:
             continue
         kname = rf["kernel"].split()[0]
         seen.add(kname)
@@ -85,7 +87,7 @@ def main(trace, bench_log, out):
     seen = set()
     for key in ("roofline", "roofline_select", "roofline_backup"):
         rf = bench.get(key)
-        if not rf or rf["kernel"].split()[0] in seen:
+        if not rf or "unit" not in rf or rf["kernel"].split()[0] in seen:
             continue
         kname = rf["kernel"].split()[0]
         seen.add(kname)

@@ -148,6 +148,7 @@ struct Trees {
                       // tree has simulations left after it) | the leaf's depth << 8
     int32_t *tree_of; // [slot]
     int32_t *depth_of; // [slot]: the queued leaf's depth (k_apply loads only the path entries it uses)
+    int32_t *slot_of;  // [tree]: its queued leaf's slot this round, -1 for none (k_round: apply by tree)
     int32_t *count;   // [0] pending leaves this round, [1] trees stopped by the select budget,
                       // [2] trees with simulations left after this round's apply
     int32_t n_trees;
@@ -1181,7 +1182,10 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
         const int p = tr.pending[i];
         if ((p & 1) != 0) {  // 1 or 3
             tr.depth_of[slot] = p >> 8;
+            tr.slot_of[i] = slot;
             tr.tree_of[slot++] = i;
+        } else {
+            tr.slot_of[i] = -1;
         }
     }
     if (tid == 0) {
@@ -1409,6 +1413,29 @@ __global__ __launch_bounds__(kWave) void k_flush1(Pool pool, Trees tr, EvalCache
         wave_memory_fence();  // the descent reads the records the apply wrote
     }
     select_wave<PY>(pool, tr, cache, stats, 0, s_row, host_leaf, tag);
+}
+
+// One round of many trees in one launch (round 5, uttt_round_hash_async): wave t applies its tree's
+// evaluation of the previous round (k_apply's body, the slot from k_scan's slot_of) and then runs the
+// tree's next descent (k_select's body). Trees are independent but for the evaluation cache, whose
+// versioned records make a probe racing another tree's insert see either the old or the new record, and a
+// hit or a miss give the same tree (a miss is evaluated later with the same values). One dispatch where
+// k_apply and k_select took two.
+template <bool PY>
+__global__ __launch_bounds__(kBlock, 4) void k_round(Pool pool, Trees tr, EvalCache cache,
+                                                  const float *__restrict__ policy, int64_t pld,
+                                                  const float *__restrict__ value, int64_t vld,
+                                                  unsigned long long *stats) {
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];
+    const int t = wave_index();
+    if (t >= tr.n_trees) return;
+    const int slot = __builtin_amdgcn_readfirstlane(tr.slot_of[t]);
+    if (slot >= 0) {
+        apply_wave(pool, tr, cache, policy, pld, value, vld, nullptr, 0, stats ? stats + kKApply * kRow : nullptr,
+                   slot, s_row[threadIdx.x >> 6]);
+        wave_memory_fence();  // the descent reads the records the apply wrote
+    }
+    select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0);
 }
 
 // -------------------------------------------------------------- hash eval --
@@ -1986,6 +2013,10 @@ struct uttt_engine {
     float *h_eval = nullptr;     // fine-grained pinned: its evaluation, read by k_apply (uttt_search_apply_host):
                                  // [rows][96] policy, [rows] value, one int32 0 (the per-copy row base)
     int64_t h_eval_rows = 0;
+    // a hash round's evaluation staged by uttt_round_hash_async, applied by the next round's k_round (or by
+    // flush_dev_apply before any other call that reads the trees); UTTT_FUSED_ROUNDS=0: separate launches
+    const float *dev_apply_policy = nullptr, *dev_apply_value = nullptr;
+    bool dev_apply_staged = false;
     int32_t host_apply_rows = 0;  // a one-tree evaluation staged by uttt_search_apply_host, applied by the next
                                   // k_flush1 (or by flush_host_apply before any other call that reads the tree)
     int32_t leaf_tag = 0;
@@ -2218,7 +2249,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->tr.leaf, max_trees)) || (rc = alloc_n(e, &e->tr.rec, max_trees)) ||
         (rc = alloc_n(e, &e->tr.path, (size_t)max_trees * kMaxDepth)) ||
         (rc = alloc_n(e, &e->tr.path_rec, (size_t)max_trees * kMaxDepth)) || (rc = alloc_n(e, &e->tr.pending, max_trees)) ||
-        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.depth_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
+        (rc = alloc_n(e, &e->tr.tree_of, max_trees)) || (rc = alloc_n(e, &e->tr.depth_of, max_trees)) ||
+        (rc = alloc_n(e, &e->tr.slot_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount * kRow)) ||
         (rc = alloc_n(e, &e->d_cache_ctr, 4 * kRow)))
@@ -2331,6 +2363,7 @@ int uttt_search_begin_mode(uttt_engine_t *e, const uttt_state_t *roots, int32_t 
     }
     HIP_TRY(hipSetDevice(e->device));
     e->host_apply_rows = 0;  // a staged evaluation of the previous search is dropped with it
+    e->dev_apply_staged = false;
     int rc = search_begin_common(e, n_trees, sims, batch);
     if (rc) return rc;
     e->tr.py = semantics == UTTT_SEMANTICS_PY ? 1 : 0;
@@ -2497,7 +2530,18 @@ static HostApplyArgs host_apply_args(uttt_engine *e) {
 
 // A staged one-tree evaluation that no k_flush1 has applied yet, applied now (any call other than
 // uttt_search_select_host that reads or restarts the tree)
+static int flush_dev_apply(uttt_engine *e) {
+    if (!e->dev_apply_staged) return UTTT_OK;
+    e->dev_apply_staged = false;
+    // the phase-3 form of uttt_search_apply: every tree's wave, the count read on the device
+    timed_launch(e, kKApply, k_apply, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), e->pool, e->tr, e->cache,
+                 e->dev_apply_policy, (int64_t)81, e->dev_apply_value, (int64_t)1, (const int32_t *)nullptr, 0,
+                 bytes_ptr(e, kKApply));
+    return check_launch();
+}
+
 static int flush_host_apply(uttt_engine *e) {
+    if (int rc = flush_dev_apply(e)) return rc;
     if (!e->host_apply_rows) return UTTT_OK;
     const HostApplyArgs a = host_apply_args(e);
     e->host_apply_rows = 0;
@@ -2666,15 +2710,63 @@ int uttt_eval_hash_dev(uttt_engine_t *e, float *policy, float *value) {
     return check_launch();
 }
 
+// the first round after a begin (nothing staged): the plain select, then this round's evaluation staged
+static int select_async_then_stage(uttt_engine *e, int32_t ring_slot, int32_t tag, float *policy, float *value) {
+    int rc = select_async_impl(e, e->h_ring + 4 * ring_slot, tag);
+    if (rc) return rc;
+    if ((rc = uttt_eval_hash_dev(e, policy, value))) return rc;
+    e->dev_apply_policy = policy;
+    e->dev_apply_value = value;
+    e->dev_apply_staged = true;
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
+}
+
 int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value) {
     if (!e || !policy || !value || ring_slot < 0 || ring_slot >= kCountRing) {
         set_error("uttt_round_hash_async: bad arguments (ring slot must be in 0..%d)", kCountRing - 1);
         return UTTT_ERR_ARG;
     }
-    int rc = select_async_impl(e, e->h_ring + 4 * ring_slot, tag);
-    if (rc) return rc;
+    static const bool fuse = [] {
+        const char *v = getenv("UTTT_FUSED_ROUNDS");
+        return !(v && v[0] == '0');
+    }();
+    if (!fuse) {
+        int rc = select_async_impl(e, e->h_ring + 4 * ring_slot, tag);
+        if (rc) return rc;
+        if ((rc = uttt_eval_hash_dev(e, policy, value))) return rc;
+        return uttt_search_apply(e, policy, 81, value, 1, 0, 1);
+    }
+    // the previous round's apply and this round's select as one k_round launch; this round's apply is staged
+    if (!e->dev_apply_staged) return select_async_then_stage(e, ring_slot, tag, policy, value);
+    if (e->phase != 1) {
+        set_error("uttt_round_hash_async: call uttt_search_begin (or apply the previous round) first");
+        return UTTT_ERR_ORDER;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->host_apply_rows) {  // (a one-tree host evaluation cannot be staged beside a round's)
+        set_error("uttt_round_hash_async: a host-staged evaluation is pending");
+        return UTTT_ERR_ORDER;
+    }
+    e->dev_apply_staged = false;
+    int rc = 0;
+    timed_launch(e, kKSelect, e->tr.py ? k_round<true> : k_round<false>, dim3(grid_waves(e->tr.n_trees)),
+                 dim3(kBlock), e->pool, e->tr, e->cache, e->dev_apply_policy, (int64_t)81, e->dev_apply_value,
+                 (int64_t)1, e->timing ? e->d_bytes : nullptr);
+    if ((rc = check_launch())) return rc;
+    timed_launch(e, kKScan, k_scan, dim3(1), dim3(1024), e->tr, e->timing ? e->d_bytes : nullptr,
+                 e->h_ring + 4 * ring_slot, tag);
+    if ((rc = check_launch())) return rc;
+    e->n_pending = -1;
+    e->phase = 3;
     if ((rc = uttt_eval_hash_dev(e, policy, value))) return rc;
-    return uttt_search_apply(e, policy, 81, value, 1, 0, 1);
+    e->dev_apply_policy = policy;
+    e->dev_apply_value = value;
+    e->dev_apply_staged = true;
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
 }
 
 static int check_tree_errors(uttt_engine *e) {
@@ -2826,6 +2918,7 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
         return UTTT_ERR_ORDER;
     }
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = flush_host_apply(e)) return rc0;  // a staged round's evaluation (uttt_round_hash_async)
     int rc = check_tree_errors(e);
     if (rc) return rc;
     const int slots = e->sp.slots;
@@ -2887,6 +2980,7 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
         return UTTT_ERR_ORDER;
     }
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = flush_host_apply(e)) return rc0;  // a staged round's evaluation (uttt_round_hash_async)
     const int slots = e->sp.slots;
     {  // d_err was reset by this move's k_begin
         TimedLaunch tl(e, kKMoveEnd);

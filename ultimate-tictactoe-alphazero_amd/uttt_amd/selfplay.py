@@ -48,8 +48,9 @@ class HashEvaluator:
         return self.policy[:n], self.value[:n]
 
     def round_async(self, engine, slot):
-        """The whole round in one C call (Engine.round_hash_async: select, scan, this evaluator, apply);
-        SelfPlay.steps then polls the returned tag in the host count ring instead of an event."""
+        """The whole round in one C call (Engine.round_hash_async: the previous round's apply and this round's
+        select as one k_round launch, scan, this evaluator; this round's apply is staged for the next call or
+        the move's end). SelfPlay.steps then polls the returned tag in the host count ring instead of an event."""
         return engine.round_hash_async(slot, self.policy, self.value)
 
 
