@@ -44,7 +44,7 @@ def main(trace, bench_log, out):
     total = sum(a[1] for a in agg.values())
     span = win[-1][1] - win[0][0]
     lines = [f"# rocprofv3 kernel trace — timed window of `{bench_log}`", "",
-             f"bench value (under rocprof): {bench['value']:.0f} sims/s; window = last {nwin} k_select dispatches "
+             f"bench value (under rocprof): {bench['value']:.0f} sims/s; window = last {nwin} {' / '.join(names)} dispatches "
              f"and everything after; span {span / 1e6:.1f} ms, kernel busy {total / 1e6:.1f} ms", "",
              "| kernel | calls | total ms | % busy | avg us | VGPR | SGPR | scratch |", "|---|---|---|---|---|---|---|---|"]
     for n, a in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
