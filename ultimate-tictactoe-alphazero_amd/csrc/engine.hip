@@ -1167,9 +1167,15 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     }
     const int per = (tr.n_trees + 1023) / 1024;
     const int b = tid * per, e = min(b + per, tr.n_trees);
+    // up to kScanPer flags per thread (4,096 trees) are loaded together and kept for the second pass (round 5:
+    // the two loops each waited for one load per tree in turn); more per thread are re-read there
+    constexpr int kScanPer = 4;
+    int held[kScanPer];
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) held[j] = b + j < e ? tr.pending[b + j] : 0;
     unsigned long long local = 0, cap = 0, mo = 0;
     for (int i = b; i < e; ++i) {
-        const int p = tr.pending[i] & 0xFF;
+        const int p = (i - b < kScanPer ? held[i - b] : tr.pending[i]) & 0xFF;
         local += p == 1 || p == 3;
         cap += p == 2;
         mo += p >= 2;
@@ -1179,7 +1185,7 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
     const unsigned long long ex = block_scan_1024(local | (cap << 21) | (mo << 42), &tot, wsum);
     int slot = (int)(ex & 0x1FFFFFull);
     for (int i = b; i < e; ++i) {
-        const int p = tr.pending[i];
+        const int p = i - b < kScanPer ? held[i - b] : tr.pending[i];
         if ((p & 1) != 0) {  // 1 or 3
             tr.depth_of[slot] = p >> 8;
             tr.slot_of[i] = slot;
