@@ -1568,6 +1568,10 @@ struct Slot {
     int32_t seed_pending;  // 1: k_finalize gave the slot a new game whose MT19937 key k_archive seeds
 };
 
+static_assert(offsetof(Slot, ply) == 40 && offsetof(Slot, live) == 44 && offsetof(Slot, finished) == 48 &&
+                  offsetof(Slot, fin_len) == 52,
+              "k_finalize reads Slot bytes 40..55 as one int4 (ply, live, finished, fin_len)");
+
 struct GameEntry {
     int64_t game;
     int64_t offset;
@@ -1851,22 +1855,28 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
     const int tid = threadIdx.x;
     const int per = (sp.slots + 1023) / 1024;
     const int b = tid * per, e = min(b + per, sp.slots);
-    // up to kFinPer slots per thread (4,096 slots) are read once, all loads in flight together, and
-    // kept in registers for the second pass; more slots per thread are re-read there
+    // the scans need a slot's live / finished / fin_len only: one 16-byte load of Slot bytes 40..55 per slot
+    // (up to kFinPer per thread, all in flight together, kept for the second pass), and the second pass
+    // reads and rewrites only the slots that change (a game just finished or the slot is free); every other
+    // slot was brought up to date by k_move_end. Round 5: the single block read and wrote every 80-byte
+    // slot through one CU (31 us per move at 4,096 slots).
     constexpr int kFinPer = 4;
-    Slot held[kFinPer];
+    int4 hot[kFinPer];
 #pragma unroll
     for (int j = 0; j < kFinPer; ++j)
-        if (b + j < e) held[j] = sp.slot[b + j];
+        if (b + j < e) hot[j] = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(sp.slot + b + j) + 40);
+    auto hot_of = [&](int i) -> int4 {
+        return i - b < kFinPer ? hot[i - b] : *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(sp.slot + i) + 40);
+    };
     long long fl = 0;
     int fr = 0, fc = 0;
     for (int i = b; i < e; ++i) {
-        const Slot sl = i - b < kFinPer ? held[i - b] : sp.slot[i];
-        if (sl.finished) {
-            fl += sl.fin_len;
+        const int4 h = hot_of(i);  // ply, live, finished, fin_len
+        if (h.z) {
+            fl += h.w;
             ++fc;
         }
-        if (!sl.live) ++fr;
+        if (!h.y) ++fr;
     }
     unsigned long long fl_tot, cnt_tot;
     const unsigned long long fl_ex = block_scan_1024((unsigned long long)fl, &fl_tot, wsum);
@@ -1880,7 +1890,9 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
     const long long fin_total = (long long)fl_tot;
     const int free_total = (int)(cnt_tot & 0xFFFFFFFFull), fin_count = (int)(cnt_tot >> 32);
     for (int i = b; i < e; ++i) {
-        Slot sl = i - b < kFinPer ? held[i - b] : sp.slot[i];
+        const int4 h = hot_of(i);
+        if (!h.z && h.y) continue;  // playing on: nothing here changes it
+        Slot sl = sp.slot[i];
         if (sl.finished) {
             if (off + sl.fin_len <= sp.arena_cap && gi < sp.games_cap) {
                 sl.fin_offset = off;
