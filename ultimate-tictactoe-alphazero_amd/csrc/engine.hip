@@ -2346,6 +2346,7 @@ int uttt_engine_set_stream(uttt_engine_t *e, void *stream) {
 int64_t uttt_engine_device_bytes(const uttt_engine_t *e) { return e ? e->bytes : 0; }
 
 static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, int32_t batch) {
+    e->dev_apply_staged = false;  // a staged round of a search that was never ended is dropped with it
     if (n_trees <= 0 || n_trees > e->max_trees) {
         set_error("n_trees %d out of range 1..%d", n_trees, e->max_trees);
         return UTTT_ERR_ARG;
@@ -2908,6 +2909,7 @@ int uttt_selfplay_move_begin(uttt_engine_t *e, int32_t *n_live) {
         int rc0 = uttt_engine_cache_clear(e);
         if (rc0) return rc0;
     }
+    e->dev_apply_staged = false;  // (a move that was never ended)
     e->moves++;
     // roots = the slots' current positions (Slot.state is the first member)
     std::vector<int32_t> live(slots);
@@ -2977,6 +2979,7 @@ int uttt_selfplay_move_begin_async(uttt_engine_t *e) {
     }
     HIP_TRY(hipSetDevice(e->device));
     const int slots = e->sp.slots;
+    e->dev_apply_staged = false;  // (a move that was never ended)
     e->tr.n_trees = slots;
     e->moves++;
     hipLaunchKernelGGL(k_begin, dim3(grid_waves(slots)), dim3(kBlock), 0, e->stream, e->pool, e->tr,
