@@ -408,14 +408,16 @@ class SelfPlay:
         return total
 
     def _lookahead(self):
-        """Rounds in flight per lane: UTTT_ROUND_LOOKAHEAD, else 2 when every lane's evaluator is cheap
+        """Rounds in flight per lane: UTTT_ROUND_LOOKAHEAD, else 3 when every lane's evaluator is cheap
         (the device hash evaluator: a round's kernels take about as long as the host's reaction to its
-        count, so with one round in flight the GPU idled between rounds), else 1 (a network round is
-        milliseconds: the host keeps up, and an empty look-ahead round would cost its 32 conv launches)."""
+        count, so with one round in flight the GPU idled between rounds; with the fused rounds three in
+        flight beat two in 3 of 3 interleaved runs, 395M against 387M sims/s,
+        profiles/r5/ab/tree_shape/), else 1 (a network round is milliseconds: the host keeps up, and an
+        empty look-ahead round would cost its 32 conv launches)."""
         env = os.environ.get("UTTT_ROUND_LOOKAHEAD")
         if env:
             return max(1, int(env))
-        return 2 if all(getattr(ln.evaluator, "cheap", False) for ln in self.lanes) else 1
+        return 3 if all(getattr(ln.evaluator, "cheap", False) for ln in self.lanes) else 1
 
     def _enqueue_round(self, ln, spec):
         """Select of one round on the lane's stream, its counts stored by the scan into a slot of the
