@@ -74,6 +74,35 @@ def network_errors():
     return res
 
 
+def search_agreement():
+    """The same 50-simulation searches (B = 8) from 400 positions with the calibrated net through the f32-level
+    evaluator and through the f16 mode: how often the most-visited root action agrees, and the mean total
+    variation distance between the two visit distributions (a network 1e-2 off moves the searches this much)."""
+    import uttt_cpp
+    from uttt_amd import BatchedSearch
+    from uttt_amd._lib import STATE_DTYPE
+    rng = np.random.default_rng(9)
+    states = []
+    while len(states) < 400:
+        s = uttt_cpp.State()
+        while not s.is_done() and len(states) < 400:
+            if rng.random() < 0.3:
+                states.append(s)
+            s = s.next(int(rng.choice(s.legal_actions())))
+    roots = np.frombuffer(b"".join(s.packed for s in states), dtype=STATE_DTYPE)
+    net = calibrated_network(os.path.join(REPO, "tests", "golden", "netcal.npz"), "cuda")
+    out = {}
+    for prec in ("f32", "f16"):
+        bs = BatchedSearch(len(states), 50)
+        bs.run(roots, FusedNetworkEvaluator(net, bs.engine, precision=prec), 50, 8)
+        out[prec] = bs.visits()
+    (v32, L), (v16, _) = out["f32"], out["f16"]
+    agree = [int(np.argmax(v32[i, :L[i]]) == np.argmax(v16[i, :L[i]])) for i in range(len(states))]
+    tv = [0.5 * float(np.abs(v32[i, :L[i]] / 50.0 - v16[i, :L[i]] / 50.0).sum()) for i in range(len(states))]
+    return {"positions": len(states), "top_action_agreement": float(np.mean(agree)), "mean_visit_tv": float(np.mean(tv)),
+            "identical_visits": float(np.mean([np.array_equal(v32[i], v16[i]) for i in range(len(states))]))}
+
+
 def timing():
     lib = _lib.load()
     net = random_network(0)
@@ -110,4 +139,5 @@ def timing():
 
 
 if __name__ == "__main__":
-    print(json.dumps({"conv": conv_errors(), "network": network_errors(), "timing_us": timing()}), flush=True)
+    print(json.dumps({"conv": conv_errors(), "network": network_errors(), "search": search_agreement(),
+                      "timing_us": timing()}), flush=True)
