@@ -208,7 +208,7 @@ def union_ms(intervals):
 
 
 def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, age, warmup, steps, evaluator,
-               cache_clear_every=0):
+               cache_clear_every=0, instrument=True):
     """Continuous self-play of `games` slots on this GPU; returns the timed-window statistics."""
     import torch
     import torch.distributed as dist
@@ -253,7 +253,18 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
 
     # the hash evaluator runs inside the engine's one-call rounds (Engine.round_hash_async): no per-round
     # Python evaluator call to wrap; its time is the engine's own dispatch-event telemetry ("hash_eval")
-    sp.set_evaluator(HashEvaluator if evaluator == "hash" else make_timed)
+    # instrument=False: no events anywhere in the timed region (the engine's per-dispatch events cost the
+    # tree-only configuration a quarter of its rate); the kernel statistics then come from
+    # a separate instrumented pass
+    if instrument:
+        sp.set_evaluator(HashEvaluator if evaluator == "hash" else make_timed)
+    else:  # no events anywhere in the timed region (no evaluator wrapper, no tower events)
+        def make_plain(eng):
+            ev = make_inner(eng)
+            if hasattr(ev, "tower_events"):
+                ev.tower_events = None
+            return ev
+        sp.set_evaluator(HashEvaluator if evaluator == "hash" else make_plain)
     # continuous self-play: rank r owns the contiguous block r of global game ids (the same
     # scheme as self_play_cpp's torchrun sharding), large enough for every game it can start
     per_rank = (age + warmup + steps + 2) * games
@@ -265,7 +276,9 @@ def run_config(net, local, rank, world, games, sims, batch, lanes, cache_log2, a
     tower_events.clear()
     rows.clear()
     sp.reset_stats()
-    sp.set_timing(True)
+    # UTTT_BENCH_KERNEL_TIMING=0: no per-dispatch events in the timed region (the value without their cost;
+    # the kernel rooflines then have no times)
+    sp.set_timing(instrument)
     rounds0, finished0, leaves0 = sp.rounds, sp.finished, sp.leaves
     if world > 1:
         dist.barrier()
@@ -550,10 +563,18 @@ def main():
 
     G, S, B = args.games, args.sims, args.batch
     net0 = random_network(0, dev) if args.net == "seed0" else calibrated_network(NETCAL, dev)
-    r = run_config(net0, local, rank, world, G, S, B, args.lanes, args.cache_log2, args.age, args.warmup, args.steps,
-                   args.evaluator, args.cache_clear_every)
+    # the measurement: K steps with no per-dispatch events in the timed region; then a separate instrumented
+    # pass (every kernel timed by its own dispatch's events, the network's forwards by events) whose statistics
+    # give the rooflines and breakdowns (UTTT_BENCH_ONE_PASS=1: one instrumented pass gives both, as in round 4)
+    one_pass = os.environ.get("UTTT_BENCH_ONE_PASS", "0") == "1"
+    r_val = run_config(net0, local, rank, world, G, S, B, args.lanes, args.cache_log2, args.age, args.warmup,
+                       args.steps, args.evaluator, args.cache_clear_every, instrument=one_pass)
+    inst_steps = args.steps if one_pass else min(args.steps, 10)
+    r = r_val if one_pass else run_config(net0, local, rank, world, G, S, B, args.lanes, args.cache_log2, args.age,
+                                          min(args.warmup, 2), inst_steps, args.evaluator, args.cache_clear_every,
+                                          instrument=True)
 
-    tot = torch.tensor([float(r["sims"]), r["elapsed"]], dtype=torch.float64,
+    tot = torch.tensor([float(r_val["sims"]), r_val["elapsed"]], dtype=torch.float64,
                        device="cpu" if args.rehearse_shared_gpu else dev)
     if world > 1:
         s = tot[:1].clone()
@@ -591,6 +612,15 @@ def main():
             rv = run_config(cfg["net"], local, 0, 1, cfg["games"], cfg["sims"], cfg["batch"], cfg["lanes"],
                             cfg["cache_log2"], cfg["age"], cfg["warmup"], cfg["steps"], cfg["evaluator"])
             sv = summarize(rv, cfg["steps"])
+            if cfg["evaluator"] == "hash" and not one_pass:
+                # the search kernels' own rate without the per-dispatch events (a quarter of it at 4,096 x 50);
+                # the rooflines below come from the instrumented pass rv
+                rv_val = run_config(cfg["net"], local, 0, 1, cfg["games"], cfg["sims"], cfg["batch"], cfg["lanes"],
+                                    cfg["cache_log2"], cfg["age"], cfg["warmup"], cfg["steps"], cfg["evaluator"],
+                                    instrument=False)
+                sv_inst = summarize(rv, cfg["steps"])
+                sv = summarize(rv_val, cfg["steps"])
+                sv["instrumented_pass"] = {k: sv_inst[k] for k in ("value", "ms_per_step")}
             sv["config"] = {k: cfg[k] for k in ("games", "sims", "batch", "lanes", "cache_log2", "age", "steps",
                                                 "evaluator")}
             sv["net"] = "calibrated (tests/golden/netcal.npz)" if key == "calibrated_net" else args.net
@@ -681,7 +711,7 @@ def main():
                 "parallelism": f"games sharded over {world} GPU(s) by contiguous global-id blocks, "
                                f"no data-path collective",
             },
-            "roofline": conv_roofline(r, args.steps) if conv else tree_rf[0],
+            "roofline": conv_roofline(r, inst_steps) if conv else tree_rf[0],
             "roofline_select": dict(tree_rf[0],
                                     latency_model={
                                         "levels_per_tree_per_launch": round(st["select_levels"]["bytes"] / lev_trees, 2),
@@ -714,7 +744,13 @@ def main():
             "breakdown_ms": {"select": round(sel["ms"], 2), "apply": round(st["apply"]["ms"], 2),
                              "scan": round(st["scan"]["ms"], 2), "move_end": round(st["move_end"]["ms"], 2),
                              "nn": round(r["nn_ms"], 2), "wall": round(r["elapsed"] * 1e3, 2)},
-            "rounds_per_step": round(r["rounds"] / args.steps, 2),
+            "rounds_per_step": round(r["rounds"] / inst_steps, 2),
+            "instrumented_pass": {"steps": inst_steps, "value": round(r["sims"] / r["elapsed"], 1),
+                                  "ms_per_step": round(r["elapsed"] / inst_steps * 1e3, 3),
+                                  "note": "value and ms_per_step above: the timed steps with no events in them; the "
+                                          "rooflines, nn, breakdown_ms and eval_cache: this separate pass, every "
+                                          "kernel timed by its own dispatch's events" if not one_pass else
+                                          "one pass: value measured with the events on"},
             "games_finished_in_timed_steps": int(r["finished"]),
             "eval_cache": (dict(r["cache"], hit_rate=round(r["cache"]["hits"] / max(r["cache"]["hits"] +
                                                                                      r["cache"]["misses"], 1), 4),
