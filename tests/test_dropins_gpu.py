@@ -192,6 +192,9 @@ def test_bench_multi_rank_path(gpu):
     assert out["n_gpus"] == 2 and out["scaling"] == "weak" and "rehearsal" in out["config"]
     # 2 ranks x 256 games x 50 sims per step, whole-job over the slowest rank's time
     assert out["value"] > 0 and abs(out["value"] * out["ms_per_step"] / 1e3 - 2 * 256 * 50) < 1e-3 * 2 * 256 * 50
+    # the value's steps run with no events in them; the kernel statistics come from a separate pass
+    ip = out["instrumented_pass"]
+    assert ip["steps"] == 2 and ip["value"] > 0 and out["roofline"]["launches"] > 0
 
 
 def test_mini_train_cycle(gpu, tmp_path, monkeypatch):
