@@ -155,7 +155,10 @@ int uttt_search_count_ptr(uttt_engine_t *eng, const int32_t **count);
  * the engine's host-visible count ring (fine-grained pinned memory, system-scope stores): the host
  * reads them once an event recorded after this call has completed, with no copy on the stream. */
 int uttt_search_select_async_to(uttt_engine_t *eng, int32_t ring_slot);
-/* The count ring: *ring = n_slots x {pending, stopped, left after apply, unused} int32, host memory. */
+/* The same, and the scan stores `tag` into word 3 of the slot after the counts (a system-scope release
+ * store): the host polls the tag instead of an event (round 5, SelfPlay's network rounds). */
+int uttt_search_select_async_tag(uttt_engine_t *eng, int32_t ring_slot, int32_t tag);
+/* The count ring: *ring = n_slots x {pending, stopped, left after apply, tag} int32, host memory. */
 int uttt_search_count_ring(uttt_engine_t *eng, const int32_t **ring, int32_t *n_slots);
 
 /* Host copies of the pending leaves (slot order) and their multiplicity k

@@ -2443,6 +2443,14 @@ int uttt_search_select_async_to(uttt_engine_t *e, int32_t ring_slot) {
     return select_async_impl(e, e->h_ring + 4 * ring_slot);
 }
 
+int uttt_search_select_async_tag(uttt_engine_t *e, int32_t ring_slot, int32_t tag) {
+    if (!e || ring_slot < 0 || ring_slot >= kCountRing) {
+        set_error("uttt_search_select_async_tag: ring slot must be in 0..%d", kCountRing - 1);
+        return UTTT_ERR_ARG;
+    }
+    return select_async_impl(e, e->h_ring + 4 * ring_slot, tag);
+}
+
 int uttt_search_count_ring(uttt_engine_t *e, const int32_t **ring, int32_t *n_slots) {
     if (!e || !ring || !n_slots) return UTTT_ERR_ARG;
     *ring = e->h_ring;

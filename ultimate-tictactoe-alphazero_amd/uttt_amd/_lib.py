@@ -76,6 +76,7 @@ SIGNATURES = {
     "uttt_selfplay_move_result": (ctypes.c_int, [_P, _I64P, _I32P]),
     "uttt_search_count_copy": (ctypes.c_int, [_P, _P]),
     "uttt_search_select_async_to": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "uttt_search_select_async_tag": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "uttt_search_count_ring": (ctypes.c_int, [_P, _P, _P]),
     "uttt_search_count_ptr": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p)]),
     "uttt_search_pending": (ctypes.c_int, [_P, _SP, _I32P]),

@@ -126,6 +126,14 @@ class Engine:
         check(self.lib.uttt_search_select_async_to(self.h, int(ring_slot)))
         self.n_pending = None
 
+    def select_async_tag(self, ring_slot):
+        """select_async_to whose scan stores a new tag into word 3 of the ring slot after the counts; returns
+        the tag (the counts are readable once the slot's word 3 holds it)."""
+        self.tag = (getattr(self, "tag", 0) + 1) & 0x7FFFFFFF
+        check(self.lib.uttt_search_select_async_tag(self.h, int(ring_slot), self.tag))
+        self.n_pending = None
+        return self.tag
+
     def count_ring(self):
         """The engine's host count ring as an (n_slots, 4) int32 numpy view of pinned host memory."""
         p, n = ctypes.c_void_p(), ctypes.c_int32()

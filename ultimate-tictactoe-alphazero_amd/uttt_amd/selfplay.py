@@ -435,13 +435,18 @@ class SelfPlay:
             # into the ring slot after the counts (no event, no torch stream context per round)
             return rc, _TagReady(buf, one_call(ln.engine, slot)), spec, buf
         with self._ctx(ln):
-            ln.engine.select_async_to(slot)
-            ev = torch.cuda.Event()
-            ev.record()
+            # readiness: the tag the scan stores into the ring slot after the counts (round 5; a torch event
+            # per round before)
+            if os.environ.get("UTTT_ROUND_EVENTS") == "1":  # the round-4 form, kept for A/B
+                ln.engine.select_async_to(slot)
+                ready = torch.cuda.Event()
+                ready.record()
+            else:
+                ready = _TagReady(buf, ln.engine.select_async_tag(slot))
             if spec:
                 p, v = ln.evaluator(None, rc)
                 ln.engine.apply(p, v)
-        return rc, ev, spec, buf
+        return rc, ready, spec, buf
 
     def run(self, game_begin, game_end, seed_base, progress=None):
         self.begin(game_begin, game_end, seed_base)
