@@ -92,9 +92,12 @@ def newest_profile(name, match):
     """The newest committed profiles/r*/<name> JSON whose fields equal `match` (PMC summaries:
     a live bench cannot read counters)."""
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", name)), reverse=True):
-        with open(f) as fh:
-            d = json.load(fh)
-        if all(d.get(k) == v for k, v in match.items()):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):  # unreadable: never let a stray file stop the measurement
+            continue
+        if isinstance(d, dict) and all(d.get(k) == v for k, v in match.items()):
             d["source"] = os.path.relpath(f, REPO)
             return d
     return None
@@ -480,8 +483,13 @@ def hbm_roofline(name, stat, trees_per_launch, pmc_name=None, evaluator=None, si
     prof = None
     if evaluator is not None:
         for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "prof_*.json")), reverse=True):
-            with open(f) as fh:
-                d = json.load(fh)
+            try:
+                with open(f) as fh:
+                    d = json.load(fh)
+            except (OSError, ValueError):  # not a kernel-trace summary of this form: skip it
+                continue
+            if not isinstance(d, dict) or "checks" not in d:
+                continue
             if (d.get("evaluator") == evaluator and d.get("trees_per_launch") == trees_per_launch
                     and d.get("sims_per_move") == sims and any(c["kernel"] == kname for c in d["checks"].values())):
                 prof = d
