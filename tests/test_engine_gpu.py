@@ -425,19 +425,33 @@ def test_fused_matches_fp32_on_trained_net(gpu, trained_net):
 
     import torch
     from uttt_amd.nnfast import FusedNetworkEvaluator
-    net, _ = trained_net
     d = golden("netcal.npz")
-    states = _rules_states(d["rules_index"])
-    fe = FusedNetworkEvaluator(net, None, max_batch=len(states))
-    p, v = fe.forward_states(states)
-    cpu = copy.deepcopy(net).cpu().eval()
+    x = torch.from_numpy(d["x"].astype(np.float32))
+    # The trained trunk is what is under test (its BatchNorm statistics and weight-derived kernel
+    # scales). How far the heads' last linear layers drive tanh / softmax into saturation on these
+    # out-of-distribution positions depends on the training run (MIOpen's algorithm choices differ
+    # between boxes), and a saturated output would hide the comparison; so those two layers are scaled
+    # by exact powers of two until the outputs are mostly unsaturated. Both sides see the same net.
+    net = copy.deepcopy(trained_net[0]).cpu().eval()
     with torch.no_grad():
-        pr, vr = cpu(torch.from_numpy(d["x"].astype(np.float32)))
+        for _ in range(30):
+            pr, vr = net(x)
+            sat_v = float(vr.abs().median()) >= 0.95
+            sat_p = float(pr.max(dim=1).values.median()) >= 0.95
+            if not (sat_v or sat_p):
+                break
+            for layer, sat in ((net.value_fc2, sat_v), (net.policy_fc, sat_p)):
+                if sat:
+                    layer.weight.mul_(0.5)
+                    layer.bias.mul_(0.5)
+    # mostly not saturated: the comparison is not hidden behind tanh / softmax clamping
+    assert float(vr.abs().median()) < 0.95 and float(pr.max(dim=1).values.median()) < 0.95
+    states = _rules_states(d["rules_index"])
+    fe = FusedNetworkEvaluator(copy.deepcopy(net).cuda().eval(), None, max_batch=len(states))
+    p, v = fe.forward_states(states)
     ep = float((p.cpu() - pr).abs().max())
     ev = float((v.cpu() - vr.reshape(-1)).abs().max())
     assert ev <= 1e-5 and ep <= 1e-5, (ep, ev)
-    # mostly not saturated: the comparison is not hidden behind tanh / softmax clamping
-    assert float(vr.abs().median()) < 0.95 and float(pr.max(dim=1).values.median()) < 0.95
 
 
 @pytest.mark.parametrize("netkind", ["seed0", "calibrated", "trained"])
