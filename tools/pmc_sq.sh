@@ -27,6 +27,8 @@ for p in "${PASSES[@]}"; do
   [ -n "$sel" ] || continue
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $sel --output-format csv -d $OUT/p$i -o t \
       -- python3 tools/diag/wino3h_variants.py $N > $OUT/p$i.log 2>&1
-  echo "pass $i rc=$?"
+  rc=$?
+  echo "pass $i rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
 done
 exit 0
