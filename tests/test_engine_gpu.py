@@ -170,6 +170,92 @@ def test_select_budget_changes_no_record(gpu, oracle_lib, budget, monkeypatch):
         assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64)), (budget, g)
 
 
+def _hash_sync_visits(gpu, roots, sims, batch):
+    """Root visits of a hash-evaluator search through the blocking round loop (select, eval, apply)."""
+    import torch
+    bs = gpu.BatchedSearch(len(roots), sims)
+    e = bs.engine
+    e.search_begin(roots, sims, batch)
+    pol = torch.zeros((len(roots), 81), dtype=torch.float32, device=bs.x.device)
+    val = torch.zeros(len(roots), dtype=torch.float32, device=bs.x.device)
+    while True:
+        n = e.select(bs.x)
+        if n == 0:
+            break
+        e.eval_hash(bs.x, n, pol, val)
+        e.apply(pol[:n], val[:n])
+    return e.root_visits()
+
+
+def _hash_round(e, r, pol, val):
+    """One uttt_round_hash_async round in ring slot r % 8; returns its [pending, stopped, left] counts."""
+    import time
+    slot = r % 8
+    tag = e.round_hash_async(slot, pol, val)
+    ring = e.count_ring()
+    t0 = time.time()
+    while int(ring[slot, 3]) != tag:
+        assert time.time() - t0 < 30, "round tag not stored"
+    return ring[slot, :3].copy()
+
+
+def test_fused_hash_rounds_and_host_flush_match_the_blocking_loop(gpu, oracle_lib):
+    """uttt_round_hash_async (k_round: the previous round's apply and the next select in one launch, the
+    round's own apply staged) gives the blocking loop's root visits on 64 trees; and on a one-tree search,
+    uttt_search_select_host / apply_host after two staged hash rounds apply the staged round first, so the
+    mixed search also ends with the blocking loop's visits."""
+    import ctypes
+
+    import torch
+    from uttt_amd import _lib
+    roots, _ = _random_positions(oracle_lib, 64, seed=29)
+    sims, batch = 50, 8
+    ref_v, ref_l = _hash_sync_visits(gpu, roots, sims, batch)
+    e = gpu.Engine(len(roots), sims)
+    dev = torch.device("cuda", e.device)
+    pol = torch.zeros((len(roots), 81), dtype=torch.float32, device=dev)
+    val = torch.zeros(len(roots), dtype=torch.float32, device=dev)
+    e.search_begin(roots, sims, batch)
+    for r in range(10 * sims):
+        if _hash_round(e, r, pol, val)[2] == 0:
+            break
+    v, L = e.root_visits()
+    assert np.array_equal(L, ref_l) and np.array_equal(v, ref_v)
+
+    # one-tree searches of every root (trees are independent without the evaluation cache, so each must
+    # end with its row of the 64-tree visits): two staged hash rounds, then the host-flush path
+    lib = _lib.load()
+    e1 = gpu.Engine(1, sims)
+    leaf = np.zeros(1, _lib.STATE_DTYPE)
+    x_hwc = np.zeros(243, np.float32)
+    mixed = 0
+    for i in range(len(roots)):
+        e1.search_begin(roots[i:i + 1], sims, batch)
+        ended = False
+        for r in range(2):
+            ended = _hash_round(e1, r, pol, val)[2] == 0
+            if ended:
+                break
+        mixed += not ended
+        for _ in range(10 * sims):
+            k, n = ctypes.c_int32(), ctypes.c_int32()
+            _lib.check(lib.uttt_search_select_host(e1.h, leaf.ctypes.data_as(ctypes.POINTER(_lib.UtttState)),
+                                                   ctypes.byref(k), ctypes.byref(n)))
+            if n.value == 0:
+                break
+            _lib.check(lib.uttt_states_input_hwc(leaf.ctypes.data_as(ctypes.POINTER(_lib.UtttState)), 1,
+                                                 x_hwc.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+            x = torch.from_numpy(np.ascontiguousarray(x_hwc.reshape(81, 3).T).reshape(1, 243)).to(dev)
+            e1.eval_hash(x, 1, pol, val)
+            p1 = np.ascontiguousarray(pol[:1].cpu().numpy())
+            v1 = np.ascontiguousarray(val[:1].cpu().numpy())
+            _lib.check(lib.uttt_search_apply_host(e1.h, ctypes.c_void_p(p1.ctypes.data), 81,
+                                                  ctypes.c_void_p(v1.ctypes.data), 1))
+        v, L = e1.root_visits()
+        assert L[0] == ref_l[i] and np.array_equal(v[0], ref_v[i]), i
+    assert mixed >= len(roots) // 2  # most searches did start the host path with a staged round
+
+
 @pytest.mark.parametrize("depth", ["2", "3"])
 def test_round_lookahead_leaves_every_round_count_readable(gpu, oracle_lib, depth, monkeypatch):
     """Rounds enqueued ahead of their count (UTTT_ROUND_LOOKAHEAD) and dropped when a lane's last game

@@ -2555,8 +2555,8 @@ static HostApplyArgs host_apply_args(uttt_engine *e) {
     return a;
 }
 
-// A staged one-tree evaluation that no k_flush1 has applied yet, applied now (any call other than
-// uttt_search_select_host that reads or restarts the tree)
+// A round's evaluation staged by uttt_round_hash_async that no k_round has applied yet, applied now (by
+// every call that reads, selects in or restarts the trees, uttt_search_select_host included)
 static int flush_dev_apply(uttt_engine *e) {
     if (!e->dev_apply_staged) return UTTT_OK;
     e->dev_apply_staged = false;
@@ -2588,6 +2588,9 @@ int uttt_search_select_host(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copie
         return UTTT_ERR_ORDER;
     }
     HIP_TRY(hipSetDevice(e->device));
+    // a round staged by uttt_round_hash_async on this one-tree search is applied first (k_flush1 applies only
+    // host-staged evaluations)
+    if (int rc0 = flush_dev_apply(e)) return rc0;
     int rc = 0, n = 0;
     for (;;) {  // the select budget may stop the tree before it queues a leaf: select again (as uttt_search_select)
         const int32_t tag = ++e->leaf_tag;
