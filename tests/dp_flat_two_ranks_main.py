@@ -1,6 +1,6 @@
 """Launched by tests/test_dropins_gpu.py under torch.distributed.run with 2 ranks sharing the box's GPU
 (gloo, as uttt_amd.distributed.init_from_env picks when ranks outnumber GPUs; not a test module):
-train_network's default GPU data-parallel form (UTTT_TRAIN_DP=flat: train.DPGraphedStep, two captured
+train_network's opt-in GPU data-parallel form (UTTT_TRAIN_DP=flat: train.DPGraphedStep, two captured
 graphs around one flat gradient all-reduce per step) on a small history with an uneven last batch. Each rank
 saves its weights and losses into argv[1]; the test checks that the replicas are identical."""
 import os
@@ -28,6 +28,52 @@ if __name__ == "__main__":
                                  dp="flat")
     torch.save({"sd": {k: t.detach().cpu() for k, t in model.state_dict().items()}, "losses": losses},
                os.path.join(sys.argv[1], f"m{rank}.pt"))
+
+    # The graphed step over 10 steps at world size 2 against a single-process emulation of the same
+    # job: per step, each rank's slice forward in train mode (BatchNorm over that slice
+    # alone), share x its loss backward, the gradients summed, one Adam step. Adam with eps = 1 (updates
+    # ~lr * m_hat, no sign amplification), calibrated network; the bound is 1e-3 of how far the weights moved.
+    from uttt_amd.model import calibrated_network
+    from uttt_amd.train import DPGraphedStep, local_slice, policy_loss_fn
+    dev = torch.device("cuda", local)
+    netcal = os.path.join(REPO, "tests", "golden", "netcal.npz")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    X = (torch.rand(64, 3, 9, 9, generator=g) > 0.5).float().to(dev)
+    P = torch.softmax(torch.randn(64, 81, generator=g), 1).to(dev)
+    V = (torch.rand(64, 1, generator=g) * 2 - 1).to(dev)
+    net = calibrated_network(netcal, dev).train()
+    opt = torch.optim.Adam(net.parameters(), lr=torch.tensor(1e-2, device=dev), eps=1.0, capturable=True, fused=True)
+    full = local_slice(torch.arange(32), rank, world)
+    step = DPGraphedStep(net, opt, X, P, V, len(full), len(full) / 32, graph=True, tune=False)
+    assert step.graph
+    ref = calibrated_network(netcal, dev).train()
+    opt_r = torch.optim.Adam(ref.parameters(), lr=1e-2, eps=1.0)
+    w0 = [q.detach().clone() for q in ref.parameters()]
+    hist = []
+    for t in range(10):
+        idx = torch.randperm(64, generator=g)[:32]
+        mine = local_slice(idx, rank, world).to(dev)
+        step.loss_sum.zero_()
+        step.step(mine, len(mine) / 32)
+        lt = step.loss_sum.clone()
+        torch.distributed.all_reduce(lt)
+        opt_r.zero_grad()
+        le = 0.0
+        for r in range(world):
+            sl = local_slice(idx, r, world).to(dev)
+            pp, pv = ref(X[sl])
+            loss = policy_loss_fn(pp, P[sl]) + torch.nn.functional.mse_loss(pv, V[sl])
+            (loss * (len(sl) / 32)).backward()
+            le += float(loss) * len(sl) / 32
+        opt_r.step()
+        lg = float(lt)
+        assert abs(lg - le) <= 1e-4 * abs(le), (t, lg, le)
+        moved = max((qe.detach() - q0).abs().max().item() for qe, q0 in zip(ref.parameters(), w0))
+        diff = max((qg.detach() - qe.detach()).abs().max().item() for qg, qe in zip(net.parameters(), ref.parameters()))
+        assert diff <= 1e-3 * moved, (t, diff, moved)
+        hist.append((round(lg, 6), round(le, 6), diff, moved))
+    if rank == 0:
+        print("DP-GRAPH-VS-EMULATION", hist, flush=True)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
     print("DP-FLAT-OK", rank, losses, flush=True)

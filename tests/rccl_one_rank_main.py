@@ -72,9 +72,44 @@ if __name__ == "__main__":
         scale = max(qb.grad.abs().max().item(), 1e-12)
         err = (qa.grad - qb.grad).abs().max().item()
         assert err <= 1e-3 * scale, (k, err, scale)
-    for _ in range(3):  # graph replays keep training (finite losses)
-        step.loss_sum.zero_()
-        step.step(i0, 1.0)
-        assert np.isfinite(float(step.loss_sum))
+
+    # Graph replays against the same phases run eagerly, over 12 steps. Adam with
+    # eps = 1 makes each update ~lr * m_hat (linear in the gradient), so rounding-level differences between
+    # the kernels MIOpen picks inside and outside a capture stay rounding-level instead of flipping
+    # lr * sign(g) updates; the calibrated (non-saturated) network; a new random slice every step (the
+    # index copy into the graph's input); the learning-rate tensor changed at step 6 (read by the replay);
+    # Adam's step counter and bias correction advance inside graph B. A replay bug (a stale flat gradient,
+    # a stale lr or step, the warm-up undo leaving state behind) moves the graph's weights by O(update)
+    # from the eager ones: the check bounds the distance at 1e-3 of how far the weights moved.
+    from uttt_amd.model import calibrated_network
+    netcal = os.path.join(REPO, "tests", "golden", "netcal.npz")
+    nets, steps, lrs = [], [], []
+    for graph in (True, False):
+        net = calibrated_network(netcal, "cuda").train()
+        lr_t = torch.tensor(1e-2, device="cuda")
+        opt = torch.optim.Adam(net.parameters(), lr=lr_t, eps=1.0, capturable=True, fused=True)
+        nets.append(net)
+        lrs.append(lr_t)
+        steps.append(DPGraphedStep(net, opt, X, P, V, 16, 1.0, graph=graph, tune=False))
+    assert steps[0].graph and not steps[1].graph
+    w0 = [q.detach().clone() for q in nets[1].parameters()]
+    gg = torch.Generator(device="cpu").manual_seed(11)
+    hist = []
+    for t in range(12):
+        if t == 6:
+            for lr_t in lrs:
+                lr_t.fill_(3e-3)
+        idx = torch.randperm(64, generator=gg)[:16].cuda()
+        for st in steps:
+            st.loss_sum.zero_()
+            st.step(idx, 1.0)
+        lg, le = float(steps[0].loss_sum), float(steps[1].loss_sum)
+        assert np.isfinite(lg) and abs(lg - le) <= 1e-4 * abs(le), (t, lg, le)
+        moved = max((qe.detach() - q0).abs().max().item() for qe, q0 in zip(nets[1].parameters(), w0))
+        diff = max((qg.detach() - qe.detach()).abs().max().item()
+                   for qg, qe in zip(nets[0].parameters(), nets[1].parameters()))
+        assert diff <= 1e-3 * moved, (t, diff, moved)
+        hist.append((round(lg, 6), round(le, 6), diff, moved))
     dist.destroy_process_group()
     print("RCCL-OK", losses, "flat-graph DP", la, "eager DDP", lb, flush=True)
+    print("GRAPH-VS-EAGER", hist, flush=True)

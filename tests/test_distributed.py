@@ -151,6 +151,25 @@ def _flat_worker(rank, world, port, out_dir):
     step.step(li, len(li) / 7)
     if rank == 0:
         torch.save({k: q.grad.clone() for k, q in model.named_parameters()}, os.path.join(out_dir, "g.pt"))
+    # train mode (BatchNorm on each rank's own slice): the all-reduced gradient of one flat step
+    mt = random_network(2).train()
+    opt_t = torch.optim.Adam(mt.parameters(), lr=1e-3)
+    step_t = train.DPGraphedStep(mt, opt_t, x, p, v, len(li), len(li) / 7, graph=False)
+    step_t.step(li, len(li) / 7)
+    tl = step_t.loss_sum.clone()
+    dist.all_reduce(tl)  # the ranks' shares -> the global mean loss
+    if rank == 0:
+        torch.save({"g": {k: q.grad.clone() for k, q in mt.named_parameters()}, "loss": float(tl)},
+                   os.path.join(out_dir, "gt.pt"))
+    # sync_buffers pools the ranks' running statistics: mean of means, E[var + mean^2] - mean^2
+    bn = mt.bn_input
+    with torch.no_grad():
+        bn.running_mean.fill_(1.0 + 2.0 * rank)
+        bn.running_var.fill_(0.5 + rank)
+    step_t.sync_buffers()
+    if rank == 0:  # ranks: means 1, 3 (mean 2); variances 0.5, 1.5 -> 1.0 + spread 1.0 = 2.0
+        assert torch.allclose(bn.running_mean, torch.full_like(bn.running_mean, 2.0)), bn.running_mean
+        assert torch.allclose(bn.running_var, torch.full_like(bn.running_var, 2.0)), bn.running_var
     # train mode through train_network(dp="flat"): 21 plies in batches of 8 (the last one 5 = 3 + 2):
     # parameters and the rank-averaged BatchNorm running statistics identical on both ranks
     model2 = random_network(1)
@@ -186,6 +205,52 @@ def test_flat_data_parallel_step_equals_single_process(tmp_path):
         scale = max(g64.abs().max().item(), 1e-12)
         own = (ref[torch.float32][k] - g64).abs().max().item()
         assert (g[k].double() - g64).abs().max().item() <= 2 * own + 1e-6 * scale, k
+    # train mode: the flat step's gradient is the sum over the ranks' slices of share x the gradient of
+    # that slice's loss with BatchNorm over the slice alone (per-rank statistics; train.DPGraphedStep)
+    # BatchNorm over 3-4 samples amplifies rounding: the single-process f32 gradient of the input conv
+    # lands 2e-4 to 2.3e-2 (of 5.4) from f64 depending on the host thread count alone, so the bound is
+    # 1e-2 of the gradient's scale, below any one rank's missing contribution (rank 1's part is 8% of it)
+    ref, loss_ref = {}, {}
+    for dt in (torch.float32, torch.float64):
+        mt = random_network(2).train().to(dt)
+        loss_ref[dt] = 0.0
+        for r in range(2):
+            lr_ = train.local_slice(torch.arange(7), r, 2)
+            pp, pv = mt(x[lr_].to(dt))
+            loss = train.policy_loss_fn(pp, p[lr_].to(dt)) + torch.nn.functional.mse_loss(pv, v[lr_].to(dt))
+            (loss * (len(lr_) / 7)).backward()
+            loss_ref[dt] += float(loss) * len(lr_) / 7
+        ref[dt] = {k: q.grad.double() for k, q in mt.named_parameters()}
+    gt = torch.load(os.path.join(tmp_path, "gt.pt"), weights_only=True)
+    l64 = loss_ref[torch.float64]
+    assert abs(gt["loss"] - l64) <= 1e-5 * abs(l64), (gt["loss"], l64)
+    for k, g64 in ref[torch.float64].items():
+        scale = max(g64.abs().max().item(), 1e-12)
+        err = (gt["g"][k].double() - g64).abs().max().item()
+        assert err <= 1e-2 * scale, (k, err, scale)
+    # train mode: the flat step's gradient is the sum over the ranks' slices of share x the gradient of
+    # that slice's loss with BatchNorm over the slice alone (per-rank statistics; train.DPGraphedStep)
+    # BatchNorm over 3-4 samples amplifies rounding: the single-process f32 gradient of the input conv
+    # lands 2e-4 to 2.3e-2 (of 5.4) from f64 depending on the host thread count alone, so the bound is
+    # 1e-2 of the gradient's scale, below any one rank's missing contribution (rank 1's part is 8% of it)
+    ref, loss_ref = {}, {}
+    for dt in (torch.float32, torch.float64):
+        mt = random_network(2).train().to(dt)
+        loss_ref[dt] = 0.0
+        for r in range(2):
+            lr_ = train.local_slice(torch.arange(7), r, 2)
+            pp, pv = mt(x[lr_].to(dt))
+            loss = train.policy_loss_fn(pp, p[lr_].to(dt)) + torch.nn.functional.mse_loss(pv, v[lr_].to(dt))
+            (loss * (len(lr_) / 7)).backward()
+            loss_ref[dt] += float(loss) * len(lr_) / 7
+        ref[dt] = {k: q.grad.double() for k, q in mt.named_parameters()}
+    gt = torch.load(os.path.join(tmp_path, "gt.pt"), weights_only=True)
+    l64 = loss_ref[torch.float64]
+    assert abs(gt["loss"] - l64) <= 1e-5 * abs(l64), (gt["loss"], l64)
+    for k, g64 in ref[torch.float64].items():
+        scale = max(g64.abs().max().item(), 1e-12)
+        err = (gt["g"][k].double() - g64).abs().max().item()
+        assert err <= 1e-2 * scale, (k, err, scale)
     m0 = torch.load(os.path.join(tmp_path, "m0.pt"), weights_only=True)
     m1 = torch.load(os.path.join(tmp_path, "m1.pt"), weights_only=True)
     for k in m0["sd"]:

@@ -157,7 +157,7 @@ def test_rccl_one_rank_data_path_and_ddp(gpu):
 
 
 def test_flat_dp_train_network_two_ranks(gpu, tmp_path):
-    """train_network under torchrun on the GPU (its default data-parallel form, UTTT_TRAIN_DP=flat: the
+    """train_network under torchrun on the GPU (the opt-in data-parallel form, UTTT_TRAIN_DP=flat: the
     per-rank step as two captured graphs around one flat gradient all-reduce), 2 ranks sharing the GPU over
     gloo, different start weights per rank (rank 0's are broadcast): identical weights, averaged BatchNorm
     running statistics and losses on both ranks (tests/dp_flat_two_ranks_main.py)."""

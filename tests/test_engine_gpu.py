@@ -116,6 +116,22 @@ def test_search_matches_oracle_random_positions(gpu, oracle_lib):
             assert visits[i].sum() == S
 
 
+def test_search_matches_oracle_large_flushes(gpu, oracle_lib):
+    """Flushes of up to 64-100 copies append k x L children per node, more than 64 scan groups of
+    the wave arg-max's tie search when L > 40 (the tie search covered 64 groups only)."""
+    core = oracle_lib
+    roots, ostates = _random_positions(core, 96, seed=41)
+    bs = gpu.BatchedSearch(len(roots), 400)
+    ev = gpu.HashEvaluator(bs.engine)
+    for (S, B) in [(400, 64), (300, 100)]:
+        bs.run(roots, ev, S, B)
+        visits, L = bs.visits()
+        for i, s in enumerate(ostates):
+            _, vi, _ = core.pv_mcts_scores_hash(s, 1.0, S, B)
+            assert np.array_equal(visits[i, :L[i]], vi), (S, B, i)
+            assert visits[i].sum() == S
+
+
 def test_selfplay_matches_reference_driver(gpu):
     """Golden games = reference self_play_cpp.play after np.random.seed(1234 + g)."""
     d = golden("selfplay.npz")

@@ -235,7 +235,8 @@ UTTT_DPP_STEP(v_max_u32, rm)
 UTTT_DPP_STEP(v_max_u32, b15)
 UTTT_DPP_STEP(v_max_u32, b31)
 // wave-uniform result: the index of the largest v, the lowest index among equal maxima
-__device__ __forceinline__ int wave_argmax(float v, int i) {
+// (cnt: the scanned child count; candidate indices are below it)
+__device__ __forceinline__ int wave_argmax(float v, int i, int cnt) {
     // the value as an order-preserving unsigned (-0 canonicalised to +0 first), so each step of the max
     // is an integer max (no float canonicalisation)
     uint32_t b = __float_as_uint(v + 0.0f);
@@ -256,8 +257,10 @@ __device__ __forceinline__ int wave_argmax(float v, int i) {
     // visited): the smallest index among the lanes holding the maximum. Lane l's candidate is its own first
     // maximum, child l + 64 g of its scan group g (i & 63 == l), so the answer is the lowest such lane of
     // the lowest group present: one ballot per group from group 0 (round 5: in place of a second 6-step DPP
-    // reduction and its wait states; usually group 0 or 1 answers)
-    for (int g = 0; g < 64; ++g) {
+    // reduction and its wait states; usually group 0 or 1 answers). Every scan group of the node is
+    // covered: a flush of k copies gives up to k x 81 children, more than 64 groups past batch 50.
+    const int ngroups = (cnt + kWave - 1) / kWave;
+    for (int g = 0; g < ngroups; ++g) {
         const uint64_t m = __ballot(b == top && (i >> 6) == g);
         if (m) return g * kWave + __builtin_ctzll(m);
     }
@@ -886,7 +889,7 @@ __device__ __forceinline__ void select_wave(Pool pool, Trees tr, EvalCache cache
                         if (cnt - c0 <= kWave) puct_group<1>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                         else puct_group<kScanGroup>(R, first, c0, cnt, sq, lane, best, bi, bw, s, pa, clk);
                     }
-                    bi = wave_argmax(best, bi);
+                    bi = wave_argmax(best, bi, cnt);
                     if (bi != kNone) {  // the winner's lane holds its record
                         const int wl = bi & (kWave - 1);
                         wr = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)bw.x, wl),
@@ -2347,6 +2350,7 @@ int64_t uttt_engine_device_bytes(const uttt_engine_t *e) { return e ? e->bytes :
 
 static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, int32_t batch) {
     e->dev_apply_staged = false;  // a staged round of a search that was never ended is dropped with it
+    e->host_apply_rows = 0;       // (and a staged one-tree evaluation)
     if (n_trees <= 0 || n_trees > e->max_trees) {
         set_error("n_trees %d out of range 1..%d", n_trees, e->max_trees);
         return UTTT_ERR_ARG;
@@ -2921,6 +2925,7 @@ int uttt_selfplay_move_begin(uttt_engine_t *e, int32_t *n_live) {
         if (rc0) return rc0;
     }
     e->dev_apply_staged = false;  // (a move that was never ended)
+    e->host_apply_rows = 0;       // (a one-tree evaluation staged by a search on this engine, never applied)
     e->moves++;
     // roots = the slots' current positions (Slot.state is the first member)
     std::vector<int32_t> live(slots);
@@ -2991,6 +2996,7 @@ int uttt_selfplay_move_begin_async(uttt_engine_t *e) {
     HIP_TRY(hipSetDevice(e->device));
     const int slots = e->sp.slots;
     e->dev_apply_staged = false;  // (a move that was never ended)
+    e->host_apply_rows = 0;       // (a one-tree evaluation staged by a search on this engine, never applied)
     e->tr.n_trees = slots;
     e->moves++;
     hipLaunchKernelGGL(k_begin, dim3(grid_waves(slots)), dim3(kBlock), 0, e->stream, e->pool, e->tr,

@@ -3,8 +3,9 @@ load the newest ./data/*.history, train ./model/best.pth for RN_EPOCHS epochs
 (batch 128, Adam 1e-3, LambdaLR), save ./model/latest.pth. Run directly it
 trains on one GPU; under `torchrun --nproc-per-node N` (backend nccl = RCCL) it
 trains data-parallel over N GPUs with the same global batch (uttt_amd.train:
-per rank two captured graphs around one flat gradient all-reduce, per-rank
-BatchNorm statistics; UTTT_TRAIN_DP=ddp for eager DDP with SyncBatchNorm).
+eager DDP with SyncBatchNorm, the reference's batch-128 statistics, by default;
+UTTT_TRAIN_DP=flat for two captured graphs per rank around one flat gradient
+all-reduce, with per-rank BatchNorm statistics).
 The dataset is resident in HBM; no DataLoader workers.
 """
 import os

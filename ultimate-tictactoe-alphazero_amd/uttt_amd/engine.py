@@ -126,10 +126,15 @@ class Engine:
         check(self.lib.uttt_search_select_async_to(self.h, int(ring_slot)))
         self.n_pending = None
 
+    def _next_tag(self):
+        """The next ring tag, kept in the int32 range the C ABI takes (a wrapped ctypes value would never
+        compare equal to the Python int the waiter holds)."""
+        return (getattr(self, "tag", 0) + 1) & 0x7FFFFFFF
+
     def select_async_tag(self, ring_slot):
         """select_async_to whose scan stores a new tag into word 3 of the ring slot after the counts; returns
         the tag (the counts are readable once the slot's word 3 holds it)."""
-        self.tag = (getattr(self, "tag", 0) + 1) & 0x7FFFFFFF
+        self.tag = self._next_tag()
         check(self.lib.uttt_search_select_async_tag(self.h, int(ring_slot), self.tag))
         self.n_pending = None
         return self.tag
@@ -187,7 +192,7 @@ class Engine:
         """A whole round with the hash evaluator in one call (uttt_round_hash_async): select, scan (the counts
         and then a new tag into ring slot ring_slot), hash evaluation of the pending leaves, apply. Returns
         the tag; the round's counts in count_ring()[ring_slot] are valid once its word 3 equals it."""
-        self.tag = getattr(self, "tag", 0) + 1
+        self.tag = self._next_tag()
         check(self.lib.uttt_round_hash_async(self.h, int(ring_slot), self.tag, ctypes.c_void_p(policy.data_ptr()),
                                              ctypes.c_void_p(value.data_ptr())))
         self.n_pending = None
