@@ -58,7 +58,7 @@ NN_FLOP_PER_STATE = 2 * nn_macs()  # 0.765 GFLOP per evaluated position (SURVEY 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60)  # ~1.8 s timed: resolution below 1%
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=50)
@@ -471,12 +471,13 @@ def fetch_factor():
 
 
 def hbm_roofline(name, stat, trees_per_launch, pmc_name=None, evaluator=None, sims=None):
-    """A tree kernel against HBM. achieved = algorithmic bytes per launch of THIS run / the kernel's rocprof
-    average duration from the committed kernel trace of the same command (profiles/r*/prof_*.json, matched
-    on evaluator, trees per launch and sims; BASELINE.md §3 'algorithmic bytes / rocprof time'), or the
-    dispatch events' average where no such trace is committed. The engine times each launch by its own
-    dispatch's events (hipExtLaunchKernelGGL); they still run ~5 us over rocprof per launch, both figures are
-    kept. traffic = PMC reads x the FETCH_SIZE factor measured on the kernels' load shape + writes."""
+    """A tree kernel against HBM. achieved = algorithmic bytes per launch of THIS run / this run's average
+    launch duration from each dispatch's own events (hipExtLaunchKernelGGL; the code being benchmarked,
+    ADVICE r5). The newest committed rocprof kernel trace of the same command (profiles/r*/prof_*.json,
+    matched on evaluator, trees per launch and sims; it may predate this build) is kept beside it as a
+    labelled secondary figure (rocprof_*), ~5 us per launch below the events. traffic = PMC reads x the
+    FETCH_SIZE factor measured on the kernels' load shape + writes; traffic_over_algo divides it by the
+    algorithmic bytes of the SAME PMC run (not of this run, whose step count and population differ)."""
     ms, launches, byts = stat["ms"], max(stat["launches"], 1), stat["bytes"]
     ev_us = ms * 1e3 / launches
     kname = name.split()[0]
@@ -498,24 +499,31 @@ def hbm_roofline(name, stat, trees_per_launch, pmc_name=None, evaluator=None, si
     rp_us = None
     if prof:
         rp_us = next(c["rocprof_avg_us"] for c in prof["checks"].values() if c["kernel"] == kname)
-    us = rp_us if rp_us else ev_us
+    us = ev_us
     achieved = (byts / launches / 1e9) / (us * 1e-6) if us > 0 else 0.0
+    rp_achieved = (byts / launches / 1e9) / (rp_us * 1e-6) if rp_us else None
     pmc = newest_profile(pmc_name, {"trees_per_launch": trees_per_launch}) if pmc_name else None
     ff = fetch_factor()
     traffic, detail = None, None
     if pmc:
         k = ff["factor"] if ff else 1.0
         traffic = round(pmc["fetch_bytes"] * k + pmc["write_bytes"])
+        pmc_algo = pmc.get("algo_bytes_per_launch_bench")
         detail = {"read_bytes_fetch_size": round(pmc["fetch_bytes"]), "write_bytes": round(pmc["write_bytes"]),
                   "read_correction": ff, "traffic_bounds": ([round(pmc["fetch_bytes"] * b + pmc["write_bytes"])
                                                              for b in ff["bounds"]] if ff else None),
+                  "algo_bytes_per_launch_pmc_run": pmc_algo,
+                  "traffic_over_algo": round(traffic / pmc_algo, 3) if pmc_algo else None,
+                  "writes_over_traffic": round(pmc["write_bytes"] / traffic, 3) if traffic else None,
                   "source": pmc["source"]}
     return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_detail": detail,
             "algo_bytes_per_launch": round(byts / launches), "avg_launch_us": round(us, 2),
-            "avg_launch_us_basis": ("rocprof kernel trace of the same command: " + prof["source"]) if prof else
-                                   "dispatch events of this run",
+            "avg_launch_us_basis": "dispatch events of this run",
             "rocprof_avg_launch_us": round(rp_us, 2) if rp_us else None,
+            "rocprof_achieved": round(rp_achieved, 2) if rp_achieved else None,
+            "rocprof_source": ("committed kernel trace of the same command (may predate this build): " +
+                               prof["source"]) if prof else None,
             "event_avg_launch_us": round(ev_us, 2), "launches": stat["launches"]}
 
 

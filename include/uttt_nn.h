@@ -88,6 +88,22 @@ int uttt_nn_conv3x3_wino3h_f16_dev(const float *x, const uint16_t *u, float u_sc
                                    const float *residual, float *y, const uint32_t *x_amax, int32_t x_amax_per_board,
                                    uint32_t *y_amax, uint32_t *amax_clear, int32_t clear_count, const int32_t *n_dev,
                                    int32_t max_boards, void *stream);
+/* The whole residual tower (n_layers convs = 2 per block of dual_network.py:28-45, n_layers a multiple
+ * of 4) as ONE persistent dataflow launch (csrc/wino3h_impl.h k_wino3t_tower): the same per-set
+ * arithmetic as uttt_nn_conv3x3_wino3h, so the same output bits, on min(*n_dev, max_boards) boards
+ * (n_dev may be NULL: max_boards boards). act: three [max_boards][81][128] activation buffers act_stride
+ * floats apart, X_even = act, t = act + act_stride, X_odd = act + 2 act_stride; block b reads X_b
+ * (X_even for even b): conv 2b: X_b -> t, conv 2b+1: t + X_b -> X_{b+1}; the final activation is
+ * X_{n_layers/2} (X_even: n_layers is a multiple of 4). The stem writes X_even.
+ * u_all: n_layers U buffers of uttt_nn_wino3h_weights back to back; u_scale_all[n_layers] (device);
+ * bias_all[n_layers][128]. stem_amax: the stem output's one bound (u32 float bits). rows: four per-board
+ * max rows of row_stride >= max_boards u32, row 0 zero on entry (left zero on exit; the per-conv
+ * kernels' rotation leaves it so too). ctl: (64 + ceil(max_boards / 7)) u32 of launch counters,
+ * zero before the first launch; each launch leaves them zero. One launch at a time per ctl. */
+int uttt_nn_tower_wino3h_dev(float *act, int64_t act_stride, const uint16_t *u_all, const float *u_scale_all,
+                             const float *bias_all, int32_t n_layers, const uint32_t *stem_amax, uint32_t *rows,
+                             int32_t row_stride, uint32_t *ctl, const int32_t *n_dev, int32_t max_boards,
+                             void *stream);
 /* Small batches: the conv's 128 output channels split over 2 workgroups per set (same output bits
  * as the persistent kernel). split: -1 automatic (default: up to 28 boards), 0 or 1 never, 2 always. */
 int uttt_nn_wino3h_set_split(int32_t split);

@@ -80,7 +80,11 @@ if __name__ == "__main__":
     # index copy into the graph's input); the learning-rate tensor changed at step 6 (read by the replay);
     # Adam's step counter and bias correction advance inside graph B. A replay bug (a stale flat gradient,
     # a stale lr or step, the warm-up undo leaving state behind) moves the graph's weights by O(update)
-    # from the eager ones: the check bounds the distance at 1e-3 of how far the weights moved.
+    # from the eager ones. Train-mode BatchNorm over 16 samples amplifies rounding: graph and eager
+    # gradients differ by ~0.1-1% of their scale (a CPU run of the same loss moves by 2e-4 to 2e-2 of it with
+    # the host thread count alone), so the checks bound (a) the distance at 5% of how far the weights moved
+    # and (b) each step's update difference at 10% of that update; a stale lr (x3.3 at step 6), step counter
+    # or gradient breaks (b) by an O(1) factor.
     from uttt_amd.model import calibrated_network
     netcal = os.path.join(REPO, "tests", "golden", "netcal.npz")
     nets, steps, lrs = [], [], []
@@ -93,6 +97,7 @@ if __name__ == "__main__":
         steps.append(DPGraphedStep(net, opt, X, P, V, 16, 1.0, graph=graph, tune=False))
     assert steps[0].graph and not steps[1].graph
     w0 = [q.detach().clone() for q in nets[1].parameters()]
+    prev = [[q.detach().clone() for q in n.parameters()] for n in nets]
     gg = torch.Generator(device="cpu").manual_seed(11)
     hist = []
     for t in range(12):
@@ -104,12 +109,18 @@ if __name__ == "__main__":
             st.loss_sum.zero_()
             st.step(idx, 1.0)
         lg, le = float(steps[0].loss_sum), float(steps[1].loss_sum)
-        assert np.isfinite(lg) and abs(lg - le) <= 1e-4 * abs(le), (t, lg, le)
+        # (the loss follows the weights' rounding-level drift: 1.2e-4 apart by step 4 on one box)
+        assert np.isfinite(lg) and abs(lg - le) <= 2e-3 * abs(le), (t, lg, le, hist)
         moved = max((qe.detach() - q0).abs().max().item() for qe, q0 in zip(nets[1].parameters(), w0))
         diff = max((qg.detach() - qe.detach()).abs().max().item()
                    for qg, qe in zip(nets[0].parameters(), nets[1].parameters()))
-        assert diff <= 1e-3 * moved, (t, diff, moved)
-        hist.append((round(lg, 6), round(le, 6), diff, moved))
+        # this step's update, graph against eager
+        inc = [[q.detach() - p0 for q, p0 in zip(n.parameters(), pr)] for n, pr in zip(nets, prev)]
+        step_e = max(d.abs().max().item() for d in inc[1])
+        step_d = max((a - b).abs().max().item() for a, b in zip(inc[0], inc[1]))
+        prev = [[q.detach().clone() for q in n.parameters()] for n in nets]
+        assert diff <= 5e-2 * moved and step_d <= 0.1 * step_e, (t, diff, moved, step_d, step_e, hist)
+        hist.append((round(lg, 6), round(le, 6), round(diff / moved, 5), round(step_d / step_e, 5)))
     dist.destroy_process_group()
     print("RCCL-OK", losses, "flat-graph DP", la, "eager DDP", lb, flush=True)
     print("GRAPH-VS-EAGER", hist, flush=True)

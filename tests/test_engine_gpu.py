@@ -849,6 +849,32 @@ def test_fused_outputs_do_not_depend_on_the_batch(gpu):
             assert torch.equal(p2[0], p0[i]) and torch.equal(v2[0], v0[i]), (conv, i)
 
 
+def test_dataflow_tower_equals_per_conv_launches(gpu):
+    """The tower as one persistent dataflow launch (uttt_nn_tower_wino3h_dev, round 6) gives the same
+    output bits as the 32 per-conv launches, for batch sizes across the 7-board group residues, a last group
+    of one set, and the engine's full 4,096; repeated launches reuse the counters (each launch leaves them
+    zero) and leave max row 0 zero for the next forward."""
+    import torch
+    from uttt_amd.model import calibrated_network
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    r = golden("rules.npz")
+    rng = np.random.RandomState(17)
+    pool = _rules_states(rng.choice(np.nonzero(r["n_legal"] > 0)[0], 4096, replace=True))
+    net = calibrated_network(NETCAL, "cuda")
+    fl = FusedNetworkEvaluator(net, None, max_batch=4096, tower="layers")
+    fd = FusedNetworkEvaluator(net, None, max_batch=4096, tower="dataflow")
+    for n in (29, 31, 35, 64, 200, 1373, 4096):
+        p0, v0 = (t.clone() for t in fl.forward_states(pool[:n]))
+        a0 = fl.buf[0][:n].clone()
+        for rep in range(2):
+            p1, v1 = fd.forward_states(pool[:n])
+            assert torch.equal(fd.buf[0][:n], a0), (n, rep)
+            assert torch.equal(p1, p0) and torch.equal(v1, v0), (n, rep)
+            torch.cuda.synchronize()
+            assert int(fd.ctl.abs().sum()) == 0, (n, rep)
+            assert int(fd.bamax[0].abs().sum()) == 0, (n, rep)
+
+
 def test_split_f16_conv_is_batch_independent(gpu):
     """Conv-level form of the same property: 64 boards convolved alone and inside a batch
     whose other boards are x1e3 / x1e-3 outliers give equal output bits (the V scale is per

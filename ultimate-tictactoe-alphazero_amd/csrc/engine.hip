@@ -474,7 +474,10 @@ __device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
         piece = floatx4_t{__uint_as_float(kp.x), __uint_as_float(kp.y), __uint_as_float(kp.z), __uint_as_float(kp.w)};
     }
     const rsrc_t r = rec_rsrc(c, (uint32_t)slot);
-    if (lane < kRecLanes) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, piece), r, 16 * lane, 0, kSc1);
+    // all 24 pieces (the padding as zeros): the record's three 128-byte lines are written whole, so none is
+    // a partial-line write at the memory side (round 6; 23 pieces left the third line 112 of 128 bytes)
+    if (lane < kRecBytes / 16)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, piece), r, 16 * lane, 0, kSc1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         st_agent(c.flag + slot, pub);
@@ -818,9 +821,10 @@ __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int firs
 // cv_row: this wave's 84-float LDS row (a cache hit's values). host_leaf (one-tree searches only): the
 // round's counts, the queued leaf and its copies go to fine-grained host memory behind `tag`, and the
 // round's device counts / slot 0 are written here (there is no k_scan launch in that form).
+// Returns the tree's pending word (wave-uniform), as stored to tr.pending[t].
 template <bool PY>
-__device__ __forceinline__ void select_wave(Pool pool, Trees tr, EvalCache cache, unsigned long long *stats, int t,
-                                            float *cv_row, HostLeaf *host_leaf, int32_t tag) {
+__device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache, unsigned long long *stats, int t,
+                                           float *cv_row, HostLeaf *host_leaf, int32_t tag) {
     const int lane = lane_id();
     TreeCtl ctl = tr.ctl[t];
     int pend = 0;
@@ -1097,6 +1101,7 @@ __device__ __forceinline__ void select_wave(Pool pool, Trees tr, EvalCache cache
             __hip_atomic_store(&host_leaf->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+    return __builtin_amdgcn_readfirstlane(pend);
 }
 
 template <bool PY>
@@ -1241,15 +1246,24 @@ __global__ __launch_bounds__(256) void k_encode(Trees tr, float *__restrict__ x,
 __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache, const float *__restrict__ policy,
                                            int64_t pld, const float *__restrict__ value, int64_t vld,
                                            const int32_t *__restrict__ rowbase, int per_copy,
-                                           unsigned long long *bytes_ctr, int slot, float *row /* LDS, 84 floats */) {
+                                           unsigned long long *bytes_ctr, int slot, float *row /* LDS, 84 floats */,
+                                           int by_tree = -1, int by_tree_depth = 0) {
     const int lane = lane_id();
     // two dependent round trips before the work: the count with this slot's tree and leaf depth
     // (tree_of / depth_of hold n_trees entries, stale past the count), then the tree's records, the
-    // path entries 0..depth (round 4: all 128 were loaded, 2.5 KB a leaf) and the slot's evaluation
-    const int cnt = tr.count[0];
-    const int t = tr.tree_of[slot < tr.n_trees ? slot : 0];
-    const int dq = tr.depth_of[slot < tr.n_trees ? slot : 0];
-    if (slot >= cnt) return;
+    // path entries 0..depth (round 4: all 128 were loaded, 2.5 KB a leaf) and the slot's evaluation.
+    // by_tree >= 0 (one-dispatch hash rounds, k_round1): the tree and its leaf's depth are given and its
+    // evaluation is row `slot` == by_tree (rows by tree, no scan)
+    int t, dq;
+    if (by_tree >= 0) {
+        t = by_tree;
+        dq = by_tree_depth;
+    } else {
+        const int cnt = tr.count[0];
+        t = tr.tree_of[slot < tr.n_trees ? slot : 0];
+        dq = tr.depth_of[slot < tr.n_trees ? slot : 0];
+        if (slot >= cnt) return;
+    }
     const LeafRec r = tr.rec[t];
     TreeCtl ctl = tr.ctl[t];
     const uttt_state_t s = tr.leaf[t];
@@ -1447,6 +1461,147 @@ __global__ __launch_bounds__(kBlock, 4) void k_round(Pool pool, Trees tr, EvalCa
     select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0);
 }
 
+// The hash evaluator's outputs for one state into row `row` (k_hash_leaves' body): bit j = ch * 81 + R * 9 + C
+// of the network input, as k_encode writes it, so the words and outputs are k_hash_eval's.
+__device__ __forceinline__ void hash_leaf_row(const uttt_state_t &s, float *__restrict__ policy, float *__restrict__ value,
+                                              int row);
+
+// One tree-only round in ONE dispatch (round 6; UTTT_ROUND_DISPATCHES=3 keeps k_round +
+// k_scan + k_hash_leaves). With the hash evaluator nothing needs the leaves in slot order, so the rows are
+// indexed by TREE: wave t applies its tree's evaluation of the previous round from row t (apply != 0 and its
+// pending word, still the previous round's, shows a queued leaf), runs the next descent (k_select's body), and
+// evaluates the leaf it queued straight into row t. The round's counts, which k_scan produced, are summed
+// per block into a partial (sc1 store) and the last block to arrive (striped arrival counters, then one top
+// counter) adds the partials, publishes them (device counts, the host ring and its tag) and resets the
+// counters for the next round. Every tree's work is k_round's in the same order, so every result is the
+// three-dispatch round's (the fused-rounds test runs both).
+constexpr int kR1Stripes = 8;
+constexpr int kR1Partial = 64;  // rctl: [0..7] stripe arrivals, [32] top, [64 + block] partials
+template <bool PY>
+__global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalCache cache, const float *apply_policy,
+                                                   const float *apply_value, float *__restrict__ policy,
+                                                   float *__restrict__ value, int apply, unsigned long long *stats,
+                                                   int32_t *host_count, int32_t tag, uint32_t *rctl) {
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];
+    __shared__ uint32_t s_cnt;
+    __shared__ int s_last;
+    const int t = wave_index();
+    const int lane = lane_id();
+    if (threadIdx.x == 0) s_cnt = 0u;
+    __syncthreads();
+    if (t < tr.n_trees) {
+        const int prev = __builtin_amdgcn_readfirstlane(tr.pending[t]);  // the previous round's, until the select
+        if (apply && (prev & 1)) {
+            apply_wave(pool, tr, cache, apply_policy, 81, apply_value, 1, nullptr, 0,
+                       stats ? stats + kKApply * kRow : nullptr, t, s_row[threadIdx.x >> 6], t, prev >> 8);
+            wave_memory_fence();  // the descent reads the records the apply wrote
+        }
+        const int p = select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0);
+        if (p & 1) {
+            wave_memory_fence();  // lane 0 stored the leaf
+            const uttt_state_t leaf = tr.leaf[t];
+            hash_leaf_row(leaf, policy, value, t);
+        }
+        const int q = p & 0xFF;
+        if (lane == 0)  // pending | stopped << 10 | left << 20 (at most kWavesPerBlock each)
+            atomicAdd(&s_cnt, (uint32_t)((q == 1 || q == 3) ? 1 : 0) | ((q == 2 ? 1u : 0u) << 10) |
+                                  ((q >= 2 ? 1u : 0u) << 20));
+    }
+    // every wave's stores (rows, records, stats atomics) complete before the block's partial is published
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(rctl + kR1Partial + b, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int st = b & (kR1Stripes - 1);
+        const uint32_t in_stripe = (uint32_t)((nb - st + kR1Stripes - 1) / kR1Stripes);
+        const int stripes = nb < kR1Stripes ? nb : kR1Stripes;
+        int last = 0;
+        if (__hip_atomic_fetch_add(rctl + st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_stripe - 1)
+            last = __hip_atomic_fetch_add(rctl + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (uint32_t)(stripes - 1);
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the last block: every partial was published before its block's arrival (sc1 loads, no stale L1 copy)
+    uint32_t c0 = 0u, c1 = 0u, c2 = 0u;
+    for (int i = threadIdx.x; i < nb; i += kBlock) {
+        const uint32_t v = __hip_atomic_load(rctl + kR1Partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c0 += v & 0x3FFu;
+        c1 += (v >> 10) & 0x3FFu;
+        c2 += v >> 20;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        c0 += __shfl_xor(c0, off);
+        c1 += __shfl_xor(c1, off);
+        c2 += __shfl_xor(c2, off);
+    }
+    __shared__ uint32_t s_sum[3][kWavesPerBlock];
+    if (lane == 0) {
+        s_sum[0][threadIdx.x >> 6] = c0;
+        s_sum[1][threadIdx.x >> 6] = c1;
+        s_sum[2][threadIdx.x >> 6] = c2;
+    }
+    // the select's slowest tree (as k_scan folds it): the max over the stripes, one per lane of wave 1
+    if (stats && threadIdx.x >= kWave && threadIdx.x < 2 * kWave) {
+        const int l = threadIdx.x - kWave;
+        unsigned long long ml = 0ull, mt = 0ull;
+        if (l < kStripes) {
+            unsigned long long *a = stats + kKSelMax * kRow + l * kStripeStride;
+            unsigned long long *bb = stats + kKSelTripMax * kRow + l * kStripeStride;
+            ml = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mt = __hip_atomic_load(bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bb, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long ol = __shfl_xor(ml, off), ot = __shfl_xor(mt, off);
+            ml = ol > ml ? ol : ml;
+            mt = ot > mt ? ot : mt;
+        }
+        if (l == 0) {
+            stats[kKSelMaxSum * kRow] += ml;
+            stats[kKSelTripMaxSum * kRow] += mt;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int n0 = 0, n1 = 0, n2 = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            n0 += (int)s_sum[0][w];
+            n1 += (int)s_sum[1][w];
+            n2 += (int)s_sum[2][w];
+        }
+        tr.count[0] = n0;
+        tr.count[1] = n1;
+        tr.count[2] = n2;
+        for (int i = 0; i < kR1Stripes; ++i) rctl[i] = 0u;
+        rctl[32] = 0u;
+        if (host_count) {
+            __hip_atomic_store(host_count + 0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_count + 1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_count + 2, n2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_count + 3, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// A one-dispatch round's staged evaluation applied by tree (flush before anything else reads the trees)
+__global__ __launch_bounds__(kBlock) void k_apply_tree(Pool pool, Trees tr, EvalCache cache, const float *policy,
+                                                       const float *value, unsigned long long *bytes_ctr) {
+    __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];
+    const int t = wave_index();
+    if (t >= tr.n_trees) return;
+    const int prev = __builtin_amdgcn_readfirstlane(tr.pending[t]);
+    if (prev & 1)
+        apply_wave(pool, tr, cache, policy, 81, value, 1, nullptr, 0, bytes_ctr, t, s_row[threadIdx.x >> 6], t,
+                   prev >> 8);
+}
+
 // -------------------------------------------------------------- hash eval --
 // Deterministic test evaluator on the NCHW rows: one wave per row; the 4
 // ballots of "x != 0" over the 243 floats are exactly the 4 hash words.
@@ -1513,10 +1668,15 @@ __device__ void root_scores(const Pool &pool, size_t base, float temperature, fl
 // device (the grid covers every tree).
 __global__ __launch_bounds__(kBlock) void k_hash_leaves(Trees tr, float *__restrict__ policy,
                                                         float *__restrict__ value) {
-    const int lane = lane_id();
     const int row = wave_index();
     if (row >= tr.count[0]) return;
     const uttt_state_t s = tr.leaf[tr.tree_of[row]];
+    hash_leaf_row(s, policy, value, row);
+}
+
+__device__ __forceinline__ void hash_leaf_row(const uttt_state_t &s, float *__restrict__ policy, float *__restrict__ value,
+                                              int row) {
+    const int lane = lane_id();
     uint32_t m[3];
     legal_mask(s, m);
     uint64_t w[4];
@@ -2038,6 +2198,8 @@ struct uttt_engine {
     // flush_dev_apply before any other call that reads the trees); UTTT_FUSED_ROUNDS=0: separate launches
     const float *dev_apply_policy = nullptr, *dev_apply_value = nullptr;
     bool dev_apply_staged = false;
+    bool dev_apply_by_tree = false;  // staged by a one-dispatch round (k_round1): rows by tree, no scan
+    uint32_t *d_r1ctl = nullptr;     // k_round1's arrival counters and per-block partials (zero between rounds)
     int32_t host_apply_rows = 0;  // a one-tree evaluation staged by uttt_search_apply_host, applied by the next
                                   // k_flush1 (or by flush_host_apply before any other call that reads the tree)
     int32_t leaf_tag = 0;
@@ -2274,7 +2436,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
         (rc = alloc_n(e, &e->tr.slot_of, max_trees)) || (rc = alloc_n(e, &e->tr.count, 4)) ||
         (rc = alloc_n(e, &e->d_scores, (size_t)max_trees * 81)) || (rc = alloc_n(e, &e->d_visits, (size_t)max_trees * 81)) ||
         (rc = alloc_n(e, &e->d_nlegal, max_trees)) || (rc = alloc_n(e, &e->d_bytes, kKernelCount * kRow)) ||
-        (rc = alloc_n(e, &e->d_cache_ctr, 4 * kRow)))
+        (rc = alloc_n(e, &e->d_cache_ctr, 4 * kRow)) ||
+        (rc = alloc_n(e, &e->d_r1ctl, (size_t)kR1Partial + (size_t)grid_waves(max_trees))))
         return fail(rc);
     if ((rc = alloc_n(e, &e->d_err, 1))) return fail(rc);
     if (hipHostMalloc((void **)&e->h_move, sizeof(int64_t) * 5, hipHostMallocCoherent) != hipSuccess) {
@@ -2298,6 +2461,8 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     if (hipMemsetAsync(e->tr.ctl, 0, sizeof(TreeCtl) * max_trees, e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_bytes, 0, sizeof(unsigned long long) * kKernelCount * kRow, e->stream) != hipSuccess ||
         hipMemsetAsync(e->d_cache_ctr, 0, sizeof(unsigned long long) * 4 * kRow, e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_r1ctl, 0, sizeof(uint32_t) * ((size_t)kR1Partial + (size_t)grid_waves(max_trees)),
+                       e->stream) != hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess) {
         set_error("engine init memset failed");
         return fail(UTTT_ERR_HIP);
@@ -2564,6 +2729,12 @@ static HostApplyArgs host_apply_args(uttt_engine *e) {
 static int flush_dev_apply(uttt_engine *e) {
     if (!e->dev_apply_staged) return UTTT_OK;
     e->dev_apply_staged = false;
+    if (e->dev_apply_by_tree) {  // a one-dispatch round's rows, by tree
+        e->dev_apply_by_tree = false;
+        timed_launch(e, kKApply, k_apply_tree, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), e->pool, e->tr, e->cache,
+                     e->dev_apply_policy, e->dev_apply_value, bytes_ptr(e, kKApply));
+        return check_launch();
+    }
     // the phase-3 form of uttt_search_apply: every tree's wave, the count read on the device
     timed_launch(e, kKApply, k_apply, dim3(grid_waves(e->tr.n_trees)), dim3(kBlock), e->pool, e->tr, e->cache,
                  e->dev_apply_policy, (int64_t)81, e->dev_apply_value, (int64_t)1, (const int32_t *)nullptr, 0,
@@ -2752,6 +2923,7 @@ static int select_async_then_stage(uttt_engine *e, int32_t ring_slot, int32_t ta
     e->dev_apply_policy = policy;
     e->dev_apply_value = value;
     e->dev_apply_staged = true;
+    e->dev_apply_by_tree = false;
     e->phase = 1;
     e->n_pending = 0;
     return UTTT_OK;
@@ -2766,6 +2938,36 @@ int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
         const char *v = getenv("UTTT_FUSED_ROUNDS");
         return !(v && v[0] == '0');
     }();
+    // round 6: the whole round in one dispatch (k_round1; UTTT_ROUND_DISPATCHES=3 keeps k_round + k_scan +
+    // k_hash_leaves)
+    static const bool one = [] {
+        const char *v = getenv("UTTT_ROUND_DISPATCHES");
+        return !(v && v[0] == '3');
+    }();
+    if (fuse && one) {
+        if (e->phase != 1) {
+            set_error("uttt_round_hash_async: call uttt_search_begin (or apply the previous round) first");
+            return UTTT_ERR_ORDER;
+        }
+        HIP_TRY(hipSetDevice(e->device));
+        if (e->host_apply_rows) {  // (a one-tree host evaluation cannot be staged beside a round's)
+            if (int rc0 = flush_host_apply(e)) return rc0;
+        }
+        if (e->dev_apply_staged && !e->dev_apply_by_tree)  // staged by a slot-order round: apply it first
+            if (int rc0 = flush_dev_apply(e)) return rc0;
+        const int apply = e->dev_apply_staged ? 1 : 0;
+        timed_launch(e, kKSelect, e->tr.py ? k_round1<true> : k_round1<false>, dim3(grid_waves(e->tr.n_trees)),
+                     dim3(kBlock), e->pool, e->tr, e->cache, e->dev_apply_policy, e->dev_apply_value, policy, value, apply,
+                     e->timing ? e->d_bytes : nullptr, e->h_ring + 4 * ring_slot, tag, e->d_r1ctl);
+        if (int rc0 = check_launch()) return rc0;
+        e->dev_apply_policy = policy;
+        e->dev_apply_value = value;
+        e->dev_apply_staged = true;
+        e->dev_apply_by_tree = true;
+        e->phase = 1;
+        e->n_pending = 0;
+        return UTTT_OK;
+    }
     if (!fuse) {
         int rc = select_async_impl(e, e->h_ring + 4 * ring_slot, tag);
         if (rc) return rc;
@@ -2798,6 +3000,7 @@ int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
     e->dev_apply_policy = policy;
     e->dev_apply_value = value;
     e->dev_apply_staged = true;
+    e->dev_apply_by_tree = false;
     e->phase = 1;
     e->n_pending = 0;
     return UTTT_OK;

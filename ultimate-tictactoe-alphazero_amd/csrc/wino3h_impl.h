@@ -80,6 +80,10 @@ constexpr int kEarlyLoad = 1 << 19;       // the chunk-after-next's inputs reque
 constexpr int kStagger = 1 << 30;         // waves 4-7 walk the 25 points from kStaggerRot on (their SIMD partners
                                           // from 0), so the partners' fold-free and fold-heavy points interleave
 constexpr int kStaggerRot = 12;
+constexpr int kHandoff = 1 << 20;         // k_wino3t_tower: every load of an activation, residual or per-board max
+                                          // another workgroup of the launch wrote, and every such store, is sc1
+                                          // (write-through, L1 bypassed): the hand-off needs no fence
+                                          // (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1)
 constexpr int kFoldPacked = 1 << 29;      // fold as inline-asm packed v_pk_add_f32 / v_pk_fma_f32 (rounds 1-3)
 
 struct Acc {
@@ -214,10 +218,12 @@ __device__ __forceinline__ BFrag load_b(rsrc_t u, int xi, int chunk, int voff) {
 // the XI-th point a wave visits: the points in order from ROT (0 in the product)
 template <int XI, int ROT>
 __host__ __device__ constexpr int pt() { return (XI + ROT) % NP; }
+// un: the weights of the workgroup's next chunk when it is another conv's (k_wino3t_tower: a set's last
+// chunk prefetches the next work item's U), else u
 template <int XI, int ROT = 0, bool HI = false>
-__device__ __forceinline__ BFrag load_b_ahead(rsrc_t u, int chunk, int voff) {
+__device__ __forceinline__ BFrag load_b_ahead(rsrc_t u, int chunk, int voff, rsrc_t un) {
     if constexpr (XI < NP) return load_b<HI>(u, pt<XI, ROT>(), chunk, voff);
-    else return load_b<HI>(u, pt<XI - NP, ROT>(), (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
+    else return load_b<HI>(un, pt<XI - NP, ROT>(), (chunk + 1) % NCH, voff);  // next chunk in this workgroup's order
 }
 
 // A fragments (V hi / lo of both row blocks) of one point
@@ -246,7 +252,7 @@ __device__ __forceinline__ AFrag load_a(const char *__restrict__ sv, int xi) {
 template <int XI, int MODE, int PF, int ROT = 0>
 __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ sv, rsrc_t u, BFrag (&bq)[PF],
                                         AFrag &a0, floatx2 (&mprev)[4], floatx2 k2, floatx2 k4, int chunk, int voff,
-                                        AFrag *a_next = nullptr) {
+                                        AFrag *a_next, rsrc_t un) {
     if constexpr (XI <= NP) {
         floatx2 m[4];
         if constexpr (XI < NP) {
@@ -255,7 +261,7 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
                 b2 = bq[0];
                 asm volatile("" : "+v"(b2.h), "+v"(b2.l));
             } else {
-                b2 = load_b_ahead<XI + PF, ROT, (MODE & kF16) != 0>(u, chunk, voff);
+                b2 = load_b_ahead<XI + PF, ROT, (MODE & kF16) != 0>(u, chunk, voff, un);
             }
             const BFrag b0 = bq[0];
             if constexpr (MODE & kNoALookahead) a0 = load_a<(MODE & kF16) != 0>(sv, pt<XI, ROT>());  // this point's V, waited for here
@@ -329,7 +335,7 @@ __device__ __forceinline__ void xi_loop(Acc (&S)[15], const char *__restrict__ s
         if constexpr (XI < NP) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) mprev[i] = m[i];
-            xi_loop<XI + 1, MODE, PF, ROT>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff, a_next);
+            xi_loop<XI + 1, MODE, PF, ROT>(S, sv, u, bq, a0, mprev, k2, k4, chunk, voff, a_next, un);
         }
     }
 }
@@ -340,7 +346,7 @@ __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restric
                                        int tid) {
     // the staged boards are consecutive: their positions are one run of rows of x
     const int rows = (n_boards - b0) * 81;
-    if constexpr (MODE & kBufferX) {
+    if constexpr (MODE & (kBufferX | kHandoff)) {
         // one resource per set whose range ends at the batch's last board: loads past it return 0,
         // so no lane branches and the compiler counts the loads exactly (precise vmcnt waits)
         const int nb = min(rows, SB * 81);
@@ -351,7 +357,8 @@ __device__ __forceinline__ void load_x(float4 (&xr)[XPT], const float *__restric
             const int i = tid + k * NT;
             const int q = i % (KC / 4), bp = i / (KC / 4);
             const int off = i < XF4 ? (bp * C + chunk * KC + 4 * q) * 4 : 0x7ffffff0;
-            const floatx4 t = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr_, off, 0, 2));
+            const floatx4 t = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(xr_, off, 0,
+                                                                                               (MODE & kHandoff) ? 16 : 2));
             xr[k] = make_float4(t.x, t.y, t.z, t.w);
         }
         return;
@@ -520,12 +527,21 @@ __device__ __forceinline__ float pow2_scale(float amax) {
 
 // V scales of the staged boards b0 .. b0+SB-1 (boards past the end: 1). x_amax holds one
 // max per board (per_board) or one bound for every board.
+template <bool SC1 = false>  // SC1: the maxima were written by other workgroups of this launch (k_wino3t_tower)
 __device__ __forceinline__ SetScale set_scale(const uint32_t *__restrict__ x_amax, int per_board, int b0, int n_boards) {
     SetScale sc;
 #pragma unroll
     for (int k = 0; k < SB; ++k) {
         const int b = b0 + k;
-        const uint32_t bits = per_board ? (b < n_boards ? x_amax[b] : 0u) : x_amax[0];
+        uint32_t bits;
+        if constexpr (SC1)
+            // (made wave-uniform again: the vector sc1 load would otherwise keep the scales in VGPRs)
+            bits = per_board ? (b < n_boards ? (uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+                                                   const_cast<uint32_t *>(x_amax) + b, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT))
+                                             : 0u)
+                             : x_amax[0];
+        else bits = per_board ? (b < n_boards ? x_amax[b] : 0u) : x_amax[0];
         sc.s[k] = pow2_scale(__builtin_bit_cast(float, bits));
     }
     return sc;
@@ -561,6 +577,17 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
         board_of[rt] = board;
         // this tile's board's V scale times su: both powers of two, so 1/x is exact
         inv[rt] = 1.0f / (sc.of(gb - 3 * h) * u_scale);
+    }
+    // kHandoff: residual loads and output stores through buffer resources with sc1 (same offsets and values)
+    // (k_wino3t_tower runs every conv through the RES form: res == nullptr makes the residual loads read
+    // nothing (an empty range) and skips the add, so a plain conv's bits are the plain kernel's)
+    [[maybe_unused]] rsrc_t yr_h, rr_h;
+    [[maybe_unused]] const bool has_res = res != nullptr;
+    if constexpr (MODE & kHandoff) {
+        const int nbytes = n_boards * 81 * C * 4;
+        yr_h = __builtin_amdgcn_make_buffer_rsrc(y, 0, nbytes, 0x00020000);
+        rr_h = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(has_res ? res : y), 0, has_res ? nbytes : 0,
+                                                 0x00020000);
     }
     // kResEarly (diagnostic): every residual load of the set's epilogue in flight before Y is formed
     floatx4 rve[2][9];
@@ -666,8 +693,13 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
             for (int ab = 0; ab < 9; ++ab) {
                 rv[ab] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
                 if (live[rt]) {
-                    const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
-                    rv[ab] = (MODE & 65536) ? __builtin_nontemporal_load(src) : *src;
+                    if constexpr (MODE & kHandoff) {
+                        rv[ab] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rr_h, (int)((off[rt] + ((ab / 3) * 9 + ab % 3) * C) * 4), 0, 16));
+                    } else {
+                        const floatx4 *src = reinterpret_cast<const floatx4 *>(res + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
+                        rv[ab] = (MODE & 65536) ? __builtin_nontemporal_load(src) : *src;
+                    }
                 }
             }
         }
@@ -697,12 +729,19 @@ __device__ __forceinline__ void set_epilogue(Acc (&S)[15], int st, const SetScal
             floatx4 v;
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = __builtin_fmaf(Y[ab][r], inv[rt], bb4[r]);
-            if constexpr (RES) v += rv[ab];
+            if constexpr (RES && (MODE & kHandoff)) {
+                if (has_res) v += rv[ab];
+            } else if constexpr (RES) {
+                v += rv[ab];
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.0f);
             floatx4 *dst = reinterpret_cast<floatx4 *>(y + off[rt] + ((ab / 3) * 9 + ab % 3) * C);
             if constexpr (MODE & 8) {  // diagnostic: no output stores (kept live)
                 asm volatile("" ::"v"(v));
+            } else if constexpr (MODE & kHandoff) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), yr_h,
+                                                       (int)((off[rt] + ((ab / 3) * 9 + ab % 3) * C) * 4), 0, 16);
             } else if constexpr (MODE & 131072) {
                 __builtin_nontemporal_store(v, dst);
             } else {
@@ -874,8 +913,8 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
             if constexpr (!(MODE & kNoALookahead)) a0 = load_a<(MODE & kF16) != 0>(sv_lane, rot);
             if constexpr (MODE & kALook2) an = load_a<(MODE & kF16) != 0>(sv_lane, (1 + rot) % NP);
             floatx2 mprev[4];
-            if ((MODE & kStagger) && rot) xi_loop<0, MODE, PF, kStaggerRot>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
-            else xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
+            if ((MODE & kStagger) && rot) xi_loop<0, MODE, PF, kStaggerRot>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an, ur);
+            else xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an, ur);
         }
         if constexpr (MODE & kEpiPrio)
             if (c == NCH - 1 && wv >= 4) __builtin_amdgcn_s_setprio(0);
@@ -893,6 +932,206 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
         lds_barrier();
         if (c == NCH - 1 && y_amax) flush_bmax(s_bmax, y_amax, set_b0(g), n_boards, tid);
         mark(g, 5, t0);
+    }
+}
+
+// ----------------------------------------------------------------------------------------------------
+// k_wino3t_tower: the whole residual tower (n_layers convs, dual_network.py:28-45 x 16 blocks) as ONE
+// persistent dataflow launch over work items (layer l, set st) instead of one launch per conv (round 6,
+// VERDICT r5 item 1). A board's layer-l+1 inputs are its own layer-l outputs, and a 7-board group's
+// two sets read and write only that group's boards, so layer l+1 of group g may start as soon as both
+// of its layer-l sets are done, whatever the other groups do. Items are handed out by a ticket counter in
+// layer-major order; an item waits (one lane polling done[g] with sc1 loads) only for the layer before it
+// of its own group, whose tickets are smaller and were taken by running workgroups: the smallest unfinished
+// ticket can always proceed, so the launch cannot deadlock whatever the residency. What this buys: no
+// launch boundary between convs, and no chip-wide phase lock (every workgroup of a per-conv launch reaches
+// its epilogue's HBM burst at the same moment, 13-18% of a launch); the second, half
+// empty round of sets of each per-conv launch disappears into the stream of items.
+//
+// Each item runs the product's set pipeline unchanged (the same chunk order, point order, fold and
+// epilogue arithmetic), so every output bit equals the per-conv kernels' and a board's outputs still
+// depend on that board alone. Hand-offs between workgroups (activations, residuals, per-board maxima)
+// are sc1 stores and sc1 loads (kHandoff); a producer signals done[g] with one agent-scope atomic add
+// after every wave's vmcnt(0) and a barrier (MI355X_MICROARCH.md, inter-workgroup visibility, row 1).
+//
+// Buffers: block b's input X_b is x0 (b even) or x1 (b odd); conv 2b: X_b -> t; conv 2b+1: t (+ X_b) ->
+// X_{b+1}. Per-board maxima: conv l reads row (l-1)%4 (the stem's one bound for l = 0), maxes into row
+// l%4 and clears its sets' boards in row (l+1)%4 for conv l+1; the last workgroup to exit clears row 0
+// for the next launch and resets the counters (ctl: [0] ticket, [32] exits, [64 + g] done per group).
+constexpr int kTowerCtlDone = 64;
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// DEFER: when the next item was already seen ready (its first chunk staged during this item), this item's
+// done signal waits until the next item's first chunk: every wave's vmcnt(0) after that chunk's staging
+// (the epilogue's stores and max atomics were issued before its loads) and the barrier closing the chunk,
+// so the store drain overlaps the next chunk's transform instead of stalling the workgroup. Safe: nothing
+// in that chunk waits for another workgroup.
+template <int MODE = kHandoff, int PF = 3, bool DEFER = false>
+__global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_stride, const uint16_t *__restrict__ u_all,
+                                                     const float *__restrict__ u_scale_all,
+                                                     const float *__restrict__ bias_all, int n_layers,
+                                                     const uint32_t *__restrict__ stem_amax, uint32_t *rows,
+                                                     int row_stride, uint32_t *ctl, int max_boards,
+                                                     const int32_t *__restrict__ n_dev) {
+    static_assert(MODE & kHandoff, "the tower's hand-offs need the sc1 forms");
+    __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
+    __shared__ uint32_t s_bmax[SB];
+    __shared__ int s_next[2];  // the next ticket, whether its dependency was seen met
+    float *const sX = reinterpret_cast<float *>(smem);
+    char *const sV = smem + XP * KC * 4;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t *const done = ctl + kTowerCtlDone;
+    int n_boards = max_boards;
+    if (n_dev) n_boards = min(n_boards, *n_dev);
+    const int nsets = n_sets(n_boards), total = n_layers * nsets;
+    constexpr int UL = NP * C * C * 2;  // u16 per layer
+    const int kq = lane >> 4;
+    const int voff = wv * 1024 + lane * 16;
+    const char *sv_lane = sV + kq * 256 + (((lane & 15) ^ (2 * kq)) * 16);
+    const int co4 = wv * 16 + 4 * (lane >> 4);
+    const floatx2 k2 = {2.0f, 2.0f}, k4 = {4.0f, 4.0f};
+    // item -> (layer, set); the layer's input, residual, output, maxima rows and weights
+    // buffers act + k * act_stride: k = 0 X_even, 1 t, 2 X_odd (offsets, not a select of pointers, which
+    // the compiler turns into a table in scratch)
+    auto buf = [&](int k) -> float * { return act + (size_t)k * act_stride; };
+    auto in_of = [&](int l) { return buf((l & 1) ? 1 : 2 * ((l >> 1) & 1)); };
+    auto res_of = [&](int l) -> float * { return (l & 1) ? buf(2 * ((l >> 1) & 1)) : nullptr; };
+    auto out_of = [&](int l) { return buf((l & 1) ? 2 - 2 * ((l >> 1) & 1) : 1); };
+    auto urs = [&](int l) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(u_all + (size_t)l * UL), 0, NP * C * C * 4,
+                                                 0x00020000);
+    };
+    auto scale_of = [&](int l, int b0) {
+        return l == 0 ? set_scale<true>(stem_amax, 0, b0, n_boards)
+                      : set_scale<true>(rows + (size_t)((l - 1) & 3) * row_stride, 1, b0, n_boards);
+    };
+    // the sets of group g (2, or 1 for a last group of <= 3 boards)
+    auto sets_in = [&](int g) { return min(2, nsets - 2 * g); };
+
+    if (tid < SB) s_bmax[tid] = 0u;
+    for (int i = fresh(tid); i < NPAD * (KC / 4); i += NT) {  // the staged layout's zero pads (never rewritten)
+        const int j = i / (KC / 4), q = i % (KC / 4);
+        const int pos = j < 50 ? (j / 10) * 10 * SR + j % 10
+                      : (j < 86 ? (((j - 50) / 9) * 10 + (j - 50) % 9 + 1) * SR : XP - 1);
+        reinterpret_cast<float4 *>(sX + pos * KC)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    Acc S[15];
+#pragma unroll
+    for (int i = 0; i < 15; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
+    float4 xr[XPT];
+    BFrag bq[PF];
+    if (tid == 0) s_next[0] = (int)atomicAdd(ctl, 1u);
+    __syncthreads();
+    int cur = uni(s_next[0]);
+    bool staged = false;  // the current item's first chunk is already staged in sX (and bq holds its U)
+    SetScale sc;
+    uint32_t nxt_raw = 0u;  // lane 0: the next ticket
+    int pending = -1;       // DEFER: the group whose done signal is still owed (uniform)
+#pragma unroll 1
+    while (cur < total) {
+        const int l = cur / nsets, st = cur - l * nsets, grp = st >> 1, h = st & 1, b0 = GB * grp + 3 * h;
+        const rsrc_t ur = urs(l);
+        if (tid == 0) nxt_raw = atomicAdd(ctl, 1u);  // returns during this item
+        if (!staged) {
+            // wait for layer l-1 of this group (one lane polls; the rest join at the barrier), then stage
+            if (tid == 0 && l > 0) {
+                const uint32_t need = (uint32_t)(l * sets_in(grp));
+                while (ld_sc1(done + grp) < need) __builtin_amdgcn_s_sleep(2);
+            }
+            __syncthreads();
+            sc = scale_of(l, b0);
+            load_x<MODE>(xr, in_of(l), b0, n_boards, 0, fresh(tid));
+#pragma unroll
+            for (int i = 0; i < PF; ++i) bq[i] = load_b(ur, i, 0, voff);
+            store_x(sX, xr, sc, fresh(tid));
+            __syncthreads();
+        }
+        // conv l+1's max row starts from zero on this set's boards (conv l+1 runs after both sets signal)
+        if (tid < SB && b0 + tid < n_boards && l + 1 < n_layers)
+            st_sc1(rows + (size_t)((l + 1) & 3) * row_stride + b0 + tid, 0u);
+        const floatx4 bb4 = *reinterpret_cast<const floatx4 *>(bias_all + (size_t)l * C + co4);
+        const float u_scale = u_scale_all[l];
+        const float *const xin = in_of(l);
+        int nxt = total, nl = l, nb0 = 0;
+        bool nready = false;
+#pragma unroll 1
+        for (int c = 0; c < NCH; ++c) {
+            if (c == NCH - 1) {  // the next item, as lane 0 polled it during chunk NCH-2 (uniform via LDS)
+                nxt = uni(s_next[0]);
+                nready = uni(s_next[1]) != 0;
+                if (nxt < total) {
+                    nl = nxt / nsets;
+                    const int nst = nxt - nl * nsets;
+                    nb0 = GB * (nst >> 1) + 3 * (nst & 1);
+                }
+            }
+            if (c + 1 < NCH) load_x<MODE>(xr, xin, b0, n_boards, c + 1, fresh(tid));
+            else if (nready) load_x<MODE>(xr, in_of(nl), nb0, n_boards, 0, fresh(tid));
+            SetScale sc_next = sc;
+            if (c == NCH - 1 && nready) sc_next = scale_of(nl, nb0);
+            if (c == NCH - 2 && tid == 0) {
+                const int t = (int)nxt_raw;
+                int ready = 0;
+                if (t < total) {
+                    const int tl = t / nsets, tg = (t - tl * nsets) >> 1;
+                    ready = tl == 0 || ld_sc1(done + tg) >= (uint32_t)(tl * sets_in(tg));
+                }
+                s_next[0] = t;
+                s_next[1] = ready;
+            }
+            transform<true, false>(sV, sX, fresh(tid), h);
+            lds_barrier();
+            if (c + 1 < NCH || nready) store_x(sX, xr, sc_next, fresh(tid));
+            if (DEFER && c == 0 && pending >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            {
+                AFrag a0 = load_a(sv_lane, 0), an;
+                floatx2 mprev[4];
+                const rsrc_t un = (c == NCH - 1 && nxt < total) ? urs(nl) : ur;
+                xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, c, voff, &an, un);
+            }
+            if (c == NCH - 1) {
+                // one epilogue instantiation for both forms (two inlined side by side spill ~84 VGPRs)
+                set_epilogue<true, MODE>(S, st, sc, u_scale, bb4, res_of(l), out_of(l), rows + (size_t)(l & 3) * row_stride,
+                                         n_boards, tid, lane, 0, s_bmax);
+            }
+            sc = sc_next;
+            lds_barrier();
+            if (DEFER && c == 0 && pending >= 0) {  // the previous item's signal (every wave drained above)
+                if (tid == 0) __hip_atomic_fetch_add(done + pending, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pending = -1;
+            }
+        }
+        flush_bmax(s_bmax, rows + (size_t)(l & 3) * row_stride, b0, n_boards, tid);
+        cur = nxt;
+        staged = nready && nxt < total;
+        if (DEFER && staged) {
+            pending = grp;  // signalled during the next item's first chunk
+        } else {
+            // publish: every wave's stores (outputs, maxima, the cleared row) complete, then one agent-scope add
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_fetch_add(done + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // exit: the last workgroup out resets the counters and clears max row 0 for the next launch
+    if (tid == 0) s_next[0] = (int)(atomicAdd(ctl + 32, 1u) == gridDim.x - 1);
+    __syncthreads();
+    if (s_next[0]) {
+        const int ngroups = (n_boards + GB - 1) / GB;
+        for (int g = tid; g < ngroups; g += NT) done[g] = 0u;
+        for (int b = tid; b < row_stride; b += NT) rows[b] = 0u;
+        if (tid == 0) {
+            ctl[0] = 0u;
+            ctl[32] = 0u;
+        }
     }
 }
 
@@ -970,7 +1209,7 @@ __global__ __launch_bounds__(64 * (8 / SPLIT)) void k_wino3s_conv(const float *_
         lds_barrier();
         AFrag a0 = load_a<(MODE & kF16) != 0>(sv_lane, 0), an;
         floatx2 mprev[4];
-        xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an);
+        xi_loop<0, MODE, PF>(S, sv_lane, ur, bq, a0, mprev, k2, k4, ch, voff, &an, ur);
         lds_barrier();  // sX and sV are rewritten by the next chunk
     }
     set_epilogue<RES, 0>(S, st, sc, u_scale, bb4, res, y, y_amax, n_boards, tid, lane, wave_base, s_bmax);

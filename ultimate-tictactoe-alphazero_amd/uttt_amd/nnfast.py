@@ -81,13 +81,21 @@ def _prepared_weights(net, dev, conv):
     sw, sb = fold_bn(net.conv_input, net.bn_input)            # (128,3,3,3)
     out = {"stem_w": sw.permute(1, 2, 3, 0).reshape(27, 128).contiguous().to(dev),
            "stem_b": sb.contiguous().to(dev), "heads": pack_heads(net, dev), "wino": []}
+    us, sus, bs = [], [], []
     for b in net.residual_blocks:
-        pair = []
         for cv, bn in ((b.conv1, b.bn1), (b.conv2, b.bn2)):
             w, bb = fold_bn(cv, bn)
             u, su = wino3h_weights(w)
-            pair.append((u.to(dev), su, bb.to(dev)))
-        out["wino"].append(tuple(pair))
+            us.append(u)
+            sus.append(su)
+            bs.append(bb.float())
+    # the tower's weights back to back (uttt_nn_tower_wino3h_dev); the per-conv entries are views of them
+    out["u_all"] = torch.stack(us).to(dev)
+    out["bias_all"] = torch.stack(bs).contiguous().to(dev)
+    out["scale_all"] = torch.tensor(sus, dtype=torch.float32, device=dev)
+    for i in range(0, len(us), 2):
+        out["wino"].append(((out["u_all"][i], sus[i], out["bias_all"][i]),
+                            (out["u_all"][i + 1], sus[i + 1], out["bias_all"][i + 1])))
     # the stem's output bound for every board: relu(b + sum of the positive weight rows), inputs 0/1
     out["stem_bound"] = float(torch.relu(out["stem_b"].double().cpu() +
                                          out["stem_w"].double().cpu().clamp_min(0).sum(0)).max())
@@ -103,12 +111,17 @@ class FusedNetworkEvaluator:
 
     precision: "f32" (default; the split-f16 tower, within 1e-5 of the fp32 DualNetwork) or "f16"
     (uttt_nn_conv3x3_wino3h_f16: one f16 product per point, ~1e-3 relative: the optional fast
-    evaluator, not the reference's numerics); None reads UTTT_NN_PRECISION (default f32)."""
+    evaluator, not the reference's numerics); None reads UTTT_NN_PRECISION (default f32).
+
+    tower: "dataflow" (default for f32) runs the 32 tower convs as ONE persistent launch
+    (uttt_nn_tower_wino3h_dev: work items (conv, set) handed out in conv-major order, each waiting only
+    for its own board group's previous conv); "layers" launches the convs one by one. Same output bits.
+    None reads UTTT_NN_TOWER."""
     needs_input = False
     device_count = True
     NROW = 4  # per-board max rows, rotated over the 32 convs (see __init__, _tower_heads)
 
-    def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None, precision=None):
+    def __init__(self, net, engine=None, max_batch=None, conv="wino3h", device=None, precision=None, tower=None):
         import os
         net = net.eval()
         if conv != "wino3h":
@@ -137,7 +150,17 @@ class FusedNetworkEvaluator:
             raise ValueError("the max-row rotation needs a multiple of 4 convolutions")
         w = _prepared_weights(net, dev, conv)
         self.stem_w, self.stem_b, self.heads, self.wino = w["stem_w"], w["stem_b"], w["heads"], w["wino"]
-        self.buf = [torch.zeros((self.max_batch, 81, 128), dtype=torch.float32, device=dev) for _ in range(3)]
+        self.u_all, self.bias_all, self.scale_all = w["u_all"], w["bias_all"], w["scale_all"]
+        self.tower = tower or os.environ.get("UTTT_NN_TOWER", "dataflow")
+        if self.tower not in ("dataflow", "layers"):
+            raise ValueError("tower must be 'dataflow' (one persistent launch) or 'layers' (a launch per conv)")
+        if self.precision == "f16":
+            self.tower = "layers"  # the dataflow kernel is the split-f16 (f32-level) form only
+        # X_even, t, X_odd of the tower as one allocation (the dataflow kernel addresses them by offset)
+        self.act = torch.zeros((3, self.max_batch, 81, 128), dtype=torch.float32, device=dev)
+        self.buf = [self.act[0], self.act[1], self.act[2]]
+        # the dataflow launch's counters (ticket, exits, done per 7-board group); zero between launches
+        self.ctl = torch.zeros(64 + (self.max_batch + 6) // 7 + 64, dtype=torch.int32, device=dev)
         # The stem's output is bounded for every board by relu(b + sum of the positive weight
         # rows) (its inputs are 0/1 planes): one scale for all boards. Conv i then reads the
         # per-board maxima of its input from row (i-1) % 4, atomically maxes its own output
@@ -205,8 +228,31 @@ class FusedNetworkEvaluator:
             self._plan = (key, calls, heads)
         return self._plan
 
+    def _tower_dataflow(self, stream, n_dev, max_boards):
+        check(self.lib.uttt_nn_tower_wino3h_dev(_p(self.act), ctypes.c_int64(self.act[0].numel()), _p(self.u_all),
+                                                _p(self.scale_all), _p(self.bias_all), self.nconv, _p(self.stem_amax),
+                                                _p(self.bamax), self.max_batch, _p(self.ctl), n_dev, int(max_boards),
+                                                stream))
+
     def _tower_heads(self, n, softmax, n_dev=None):
         stream = self._stream()
+        if self.tower == "dataflow" and (n_dev is not None or n > 28):
+            # one persistent launch for the whole tower (small host-count batches keep the per-conv kernels'
+            # channel split); the final activation is X_even = buf[0]
+            if self.tower_events is not None:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            self._tower_dataflow(stream, n_dev, self.max_batch if n_dev is not None else n)
+            if self.tower_events is not None:
+                ev1.record()
+                self.tower_events.append((n, ev0, ev1))
+            if n_dev is not None:
+                check(self.lib.uttt_nn_heads_dev(_p(self.buf[0]), _p(self.heads), n_dev, self.max_batch,
+                                                 _p(self.policy), _p(self.value), 1 if softmax else 0, stream))
+                return self.policy, self.value
+            check(self.lib.uttt_nn_heads(_p(self.buf[0]), _p(self.heads), n, _p(self.policy), _p(self.value),
+                                         1 if softmax else 0, stream))
+            return self.policy[:n], self.value[:n]
         if n_dev is not None:
             _, calls, heads = self._dev_plan(stream, n_dev)
             if self.tower_events is not None:
