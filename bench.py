@@ -344,18 +344,28 @@ def conv_roofline(r, steps):
     boards_per_launch = boards / len(r["tower"])
     flop = CONV_EXEC_FLOP[conv] * boards_per_launch
     achieved = flop / (avg_us * 1e-6) / 1e12
-    pmc = newest_profile("pmc_conv.json", {"kernel": "k_wino3h_conv"}) if conv == "wino3h" else None
+    dataflow = conv == "wino3h" and os.environ.get("UTTT_NN_TOWER", "layers") == "dataflow"
+    kname = "k_wino3t_tower" if dataflow else "k_wino3h_conv"
+    pmc = newest_profile("pmc_conv.json", {"kernel": kname}) if conv == "wino3h" else None
     traffic = round(pmc["hbm_bytes_per_board"] * boards_per_launch) if pmc else None
     algo_bytes = CONV_BYTES_PER_BOARD * boards_per_launch + U_BYTES_PER_SET // (2 if conv == "wino3h_f16" else 1)
-    return {"kernel": f"k_{conv}_conv (residual-tower 3x3 conv, Winograd F(3x3,3x3) on the "
-                      f"{'f16 MFMA, 3-term split-f16 products, f32 accumulation' if conv == 'wino3h' else 'f32 MFMA'})",
+    arith = 'f16 MFMA, 3-term split-f16 products, f32 accumulation' if conv == 'wino3h' else 'f16 MFMA, one product'
+    label = (f"k_wino3t_tower (the residual tower's 32 3x3 convs as ONE persistent dataflow launch, Winograd "
+             f"F(3x3,3x3) on the {arith}; per conv-equivalent: a launch's duration / 32)" if dataflow else
+             f"k_wino3h_conv (residual-tower 3x3 conv, Winograd F(3x3,3x3) on the {arith})")
+    return {"kernel": label,
             "bound": "mfma", "achieved": round(achieved, 2), "peak": CONV_PEAK[conv], "unit": "TFLOP/s",
             "frac": round(achieved / CONV_PEAK[conv], 4),
             "chip_achieved": round(chip_tflops, 2), "chip_frac": round(chip_tflops / CONV_PEAK[conv], 4),
             "conv_launch_ms_per_step": round(ms / steps, 3), "ms_per_step": round(r["elapsed"] / steps * 1e3, 3),
-            "frac_basis": "frac: per launch (HIP events around a forward's 32 launches on its lane's stream; the "
-                          "other lane's launches share the CUs meanwhile); chip_frac: all conv flops of the timed "
-                          "steps / their wall time (conv_launch_ms_per_step / ms_per_step = the lanes' overlap)",
+            "frac_basis": ("frac: per conv-equivalent (HIP events around each forward's tower launch on its lane's "
+                           "stream, / 32; the other lane's launches share the CUs meanwhile)" if dataflow else
+                           "frac: per launch (HIP events around a forward's 32 launches on its lane's stream; the "
+                           "other lane's launches share the CUs meanwhile)") +
+                          "; chip_frac: all conv flops of the timed steps / their wall time (conv_launch_ms_per_step / "
+                          "ms_per_step = the lanes' overlap)",
+            "tower_launches": len(r["tower"]) if dataflow else None,
+            "tower_avg_launch_us": round(ms * 1e3 / len(r["tower"]), 1) if dataflow else None,
             "traffic": traffic,
             "traffic_detail": ({k: pmc[k] for k in ("hbm_bytes_per_board", "fetch_bytes_per_board_x2",
                                                     "write_bytes_per_board", "source") if k in pmc} if pmc else None),
@@ -414,6 +424,36 @@ def isolated_conv(net, boards_list, reps=20):
     return {"unit": "TFLOP/s", "peak": CONV_PEAK["wino3h"], "points": out,
             "basis": "one launch at a time, no other lane (block 8 conv1 weights, random post-ReLU inputs, plain and "
                      "residual forms alternating); the headline roofline above is the in-bench figure"}
+
+
+def isolated_tower(net, boards_list, reps=10):
+    """The dataflow tower (k_wino3t_tower, UTTT_NN_TOWER=dataflow) alone on the GPU after the timed region:
+    HIP events around `reps` launches over n boards' stem outputs (opening positions), per conv-equivalent
+    (launch / 32) beside the per-conv kernel's isolated figure."""
+    import torch
+    import uttt_amd
+    from uttt_amd.nnfast import FusedNetworkEvaluator
+    out = []
+    for n in boards_list:
+        fe = FusedNetworkEvaluator(net, None, max_batch=n, tower="dataflow")
+        fe.forward_states(uttt_amd.initial_states(n))
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for _ in range(2):
+            fe._tower_dataflow(stream, None, n)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fe._tower_dataflow(stream, None, n)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        tf = CONV_EXEC_FLOP["wino3h"] * 32 * n / (us * 1e-6) / 1e12
+        out.append({"boards": n, "avg_launch_us": round(us, 1), "per_conv_us": round(us / 32, 2),
+                    "achieved": round(tf, 2), "frac": round(tf / CONV_PEAK["wino3h"], 4)})
+        del fe
+        torch.cuda.empty_cache()
+    return {"unit": "TFLOP/s", "peak": CONV_PEAK["wino3h"], "points": out,
+            "basis": "one tower launch at a time, no other lane (opening positions' stem outputs, the run's network)"}
 
 
 # Measured ceiling of the L2 -> CU vector-memory path for 16-byte lane-linear loads, every CU
@@ -671,6 +711,8 @@ def main():
     if world == 1 and not args.no_isolated and r["conv"] == "wino3h" and r["tower"]:
         nb = round(sum(n for n, _ in r["tower"]) / len(r["tower"]))
         iso = isolated_conv(net0, [nb, 16384])
+        # the optional dataflow tower alone (the two-lane headline keeps the per-conv launches: DESIGN §5)
+        iso["tower_dataflow"] = isolated_tower(net0, [nb, 16384])
 
     if rank == 0:
         value = total_sims / max_elapsed

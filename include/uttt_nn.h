@@ -98,12 +98,15 @@ int uttt_nn_conv3x3_wino3h_f16_dev(const float *x, const uint16_t *u, float u_sc
  * u_all: n_layers U buffers of uttt_nn_wino3h_weights back to back; u_scale_all[n_layers] (device);
  * bias_all[n_layers][128]. stem_amax: the stem output's one bound (u32 float bits). rows: four per-board
  * max rows of row_stride >= max_boards u32, row 0 zero on entry (left zero on exit; the per-conv
- * kernels' rotation leaves it so too). ctl: (64 + ceil(max_boards / 7)) u32 of launch counters,
- * zero before the first launch; each launch leaves them zero. One launch at a time per ctl. */
+ * kernels' rotation leaves it so too). ctl: two blocks of uttt_nn_tower_ctl_words(row_stride) u32
+ * launch counters, zero before the first launch; consecutive launches on one ctl alternate parity 0, 1
+ * (a launch resets the other block for the next). One launch at a time per ctl. Workgroups run at most
+ * UTTT_TOWER_ITEMS work items each (default 0: persistent, one workgroup per CU). */
 int uttt_nn_tower_wino3h_dev(float *act, int64_t act_stride, const uint16_t *u_all, const float *u_scale_all,
                              const float *bias_all, int32_t n_layers, const uint32_t *stem_amax, uint32_t *rows,
-                             int32_t row_stride, uint32_t *ctl, const int32_t *n_dev, int32_t max_boards,
-                             void *stream);
+                             int32_t row_stride, uint32_t *ctl, int32_t parity, const int32_t *n_dev,
+                             int32_t max_boards, void *stream);
+int32_t uttt_nn_tower_ctl_words(int32_t max_boards);
 /* Small batches: the conv's 128 output channels split over 2 workgroups per set (same output bits
  * as the persistent kernel). split: -1 automatic (default: up to 28 boards), 0 or 1 never, 2 always. */
 int uttt_nn_wino3h_set_split(int32_t split);

@@ -600,10 +600,12 @@ def test_fused_selfplay_lanes_are_bit_identical(gpu):
     from uttt_amd.nnfast import FusedNetworkEvaluator
     net = calibrated_network(NETCAL, "cuda")
     out = []
-    for lanes, cache, asy in ((1, 0, True), (1, 16, True), (2, 16, True), (2, 16, False)):
+    # the last two: the tower as one dataflow launch per forward (round 6), the count read on the device
+    for lanes, cache, asy, tower in ((1, 0, True, "layers"), (1, 16, True, "layers"), (2, 16, True, "layers"),
+                                     (2, 16, False, "layers"), (1, 0, True, "dataflow"), (2, 16, True, "dataflow")):
         sp = gpu.SelfPlay(16, 50, 8, 1.0, lanes=lanes, cache_log2=cache)
         sp.async_rounds = asy
-        sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng))
+        sp.set_evaluator(lambda eng: FusedNetworkEvaluator(net, eng, tower=tower))
         sp.run(0, 12, 4321)
         out.append(sp.records())
         if cache:
@@ -852,8 +854,8 @@ def test_fused_outputs_do_not_depend_on_the_batch(gpu):
 def test_dataflow_tower_equals_per_conv_launches(gpu):
     """The tower as one persistent dataflow launch (uttt_nn_tower_wino3h_dev, round 6) gives the same
     output bits as the 32 per-conv launches, for batch sizes across the 7-board group residues, a last group
-    of one set, and the engine's full 4,096; repeated launches reuse the counters (each launch leaves them
-    zero) and leave max row 0 zero for the next forward."""
+    of one set, and the engine's full 4,096; repeated launches alternate the two counter blocks (each launch
+    resets the block the next one uses) and leave max row 0 zero for the next forward."""
     import torch
     from uttt_amd.model import calibrated_network
     from uttt_amd.nnfast import FusedNetworkEvaluator
@@ -871,7 +873,8 @@ def test_dataflow_tower_equals_per_conv_launches(gpu):
             assert torch.equal(fd.buf[0][:n], a0), (n, rep)
             assert torch.equal(p1, p0) and torch.equal(v1, v0), (n, rep)
             torch.cuda.synchronize()
-            assert int(fd.ctl.abs().sum()) == 0, (n, rep)
+            half = fd.ctl.numel() // 2  # the block the next launch uses was reset by this one
+            assert int(fd.ctl[fd.ctl_parity * half:(fd.ctl_parity + 1) * half].abs().sum()) == 0, (n, rep)
             assert int(fd.bamax[0].abs().sum()) == 0, (n, rep)
 
 

@@ -8,7 +8,8 @@ read traffic. Algorithmic bytes per board and conv: read x (41.5 KB), write y (4
 every second conv read the residual (41.5 KB); the transformed weights (1.6 MB per launch) are
 shared by all boards.
 
-usage: pmc_conv_summary.py PMC_DIR N_BOARDS OUT.json
+usage: pmc_conv_summary.py PMC_DIR N_BOARDS OUT.json [KERNEL [CONVS_PER_DISPATCH]]
+(round 6: KERNEL k_wino3t_tower, 32 convs per dispatch: the per-board figures are per conv, as before)
 """
 import csv
 import json
@@ -22,14 +23,15 @@ def per_launch(path, counter, kernel="k_wino3h_conv"):
     return sum(v) / len(v), len(v)
 
 
-def main(d, n, out):
-    n = int(n)
-    fetch, nf = per_launch(f"{d}/p1/t_counter_collection.csv", "FETCH_SIZE")
-    write, nw = per_launch(f"{d}/p2/t_counter_collection.csv", "WRITE_SIZE")
+def main(d, n, out, kernel="k_wino3h_conv", convs=1):
+    n = int(n) * int(convs)  # board-convs per dispatch
+    fetch, nf = per_launch(f"{d}/p1/t_counter_collection.csv", "FETCH_SIZE", kernel)
+    write, nw = per_launch(f"{d}/p2/t_counter_collection.csv", "WRITE_SIZE", kernel)
     algo = 81 * 128 * 4 * 2.5
     res = {
-        "kernel": "k_wino3h_conv",
-        "boards_per_launch": n,
+        "kernel": kernel,
+        "convs_per_dispatch": int(convs),
+        "boards_per_launch": int(n) // int(convs),
         "launches_averaged": [nf, nw],
         "fetch_bytes_per_board_raw": fetch * 1024 / n,
         "fetch_bytes_per_board_x2": 2 * fetch * 1024 / n,
@@ -47,4 +49,4 @@ def main(d, n, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:])

@@ -231,43 +231,51 @@ int uttt_nn_conv3x3_wino3h_f16_dev(const float *x, const uint16_t *u, float u_sc
 
 int uttt_nn_tower_wino3h_dev(float *act, int64_t act_stride, const uint16_t *u_all, const float *u_scale_all,
                              const float *bias_all, int32_t n_layers, const uint32_t *stem_amax, uint32_t *rows,
-                             int32_t row_stride, uint32_t *ctl, const int32_t *n_dev, int32_t max_boards,
-                             void *stream) {
+                             int32_t row_stride, uint32_t *ctl, int32_t parity, const int32_t *n_dev,
+                             int32_t max_boards, void *stream) {
     if (!act || act_stride < (int64_t)max_boards * 81 * 128 || !u_all || !u_scale_all || !bias_all || !stem_amax ||
-        !rows || !ctl || n_layers <= 0 || n_layers % 4 != 0 || max_boards < 0 || row_stride < max_boards) {
+        !rows || !ctl || n_layers <= 0 || n_layers % 4 != 0 || max_boards < 0 || row_stride < max_boards ||
+        (parity != 0 && parity != 1)) {
         set_error("uttt_nn_tower_wino3h_dev: bad arguments (three activation buffers of max_boards boards act_stride "
-                  "floats apart, n_layers a positive multiple of 4, row_stride >= max_boards)");
+                  "floats apart, n_layers a positive multiple of 4, row_stride >= max_boards, parity 0 or 1)");
         return UTTT_ERR_ARG;
     }
     if (max_boards == 0) return UTTT_OK;
-    // one persistent workgroup per CU: items are handed out by the ticket counter
-    static int cus = 0;
-    if (cus <= 0) {
+    // items per workgroup (UTTT_TOWER_ITEMS; 0: one persistent workgroup per CU, every item)
+    static int items = -1, cus = 0;
+    if (items < 0) {
+        const char *e = getenv("UTTT_TOWER_ITEMS");
+        items = (e && *e) ? atoi(e) : 0;
+        if (items < 0) items = 0;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
     }
     const int max_items = n_layers * wino3h::n_sets(max_boards);
-    const dim3 grid((unsigned)(max_items < cus ? max_items : cus));
-    static int defer = -1;  // UTTT_TOWER_DEFER=0: signal every item at its end (A/B)
-    if (defer < 0) {
-        const char *e = getenv("UTTT_TOWER_DEFER");
-        defer = (e && *e == '0') ? 0 : 1;
+    int per = items, wgs;
+    if (per == 0) {
+        wgs = max_items < cus ? max_items : cus;
+        per = 1 << 30;
+    } else {
+        wgs = (max_items + per - 1) / per;
     }
-#define UTTT_TOWER(D)                                                                                                  \
-    hipLaunchKernelGGL((wino3h::k_wino3t_tower<wino3h::kHandoff, 3, D>), grid, dim3(wino3h::NT), 0, (hipStream_t)stream, \
-                       act, (int64_t)act_stride, u_all, u_scale_all, bias_all, (int)n_layers, stem_amax, rows,          \
-                       (int)row_stride, ctl, (int)max_boards, n_dev)
-    if (defer) UTTT_TOWER(true);
-    else UTTT_TOWER(false);
-#undef UTTT_TOWER
+    hipLaunchKernelGGL((wino3h::k_wino3t_tower<wino3h::kHandoff>), dim3((unsigned)wgs), dim3(wino3h::NT), 0,
+                       (hipStream_t)stream, act, (int64_t)act_stride, u_all, u_scale_all, bias_all, (int)n_layers,
+                       stem_amax, rows, (int)row_stride, ctl, (int)uttt_nn_tower_ctl_words(row_stride), (int)parity, per,
+                       (int)max_boards, n_dev);
     hipError_t r = hipGetLastError();
     if (r != hipSuccess) {
         set_error("k_wino3t_tower launch: %s", hipGetErrorString(r));
         return UTTT_ERR_HIP;
     }
     return UTTT_OK;
+}
+
+int32_t uttt_nn_tower_ctl_words(int32_t max_boards) {
+    // one block: ticket [0], items done [32], done[g] [64 + g] for ceil(max_boards / 7) groups; padded to 32
+    const int32_t w = wino3h::kTowerCtlDone + (max_boards + wino3h::GB - 1) / wino3h::GB;
+    return (w + 31) / 32 * 32;
 }
 
 int uttt_nn_wino3h_set_split(int32_t split) {

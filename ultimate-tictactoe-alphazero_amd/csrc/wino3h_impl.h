@@ -956,8 +956,7 @@ __global__ __launch_bounds__(NT) void k_wino3h_conv(const float *__restrict__ x,
 //
 // Buffers: block b's input X_b is x0 (b even) or x1 (b odd); conv 2b: X_b -> t; conv 2b+1: t (+ X_b) ->
 // X_{b+1}. Per-board maxima: conv l reads row (l-1)%4 (the stem's one bound for l = 0), maxes into row
-// l%4 and clears its sets' boards in row (l+1)%4 for conv l+1; the last workgroup to exit clears row 0
-// for the next launch and resets the counters (ctl: [0] ticket, [32] exits, [64 + g] done per group).
+// l%4 and clears its sets' boards in row (l+1)%4 for conv l+1; max row 0 is cleared at the launch's end.
 constexpr int kTowerCtlDone = 64;
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
     return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -967,18 +966,24 @@ __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// DEFER: when the next item was already seen ready (its first chunk staged during this item), this item's
-// done signal waits until the next item's first chunk: every wave's vmcnt(0) after that chunk's staging
-// (the epilogue's stores and max atomics were issued before its loads) and the barrier closing the chunk,
-// so the store drain overlaps the next chunk's transform instead of stalling the workgroup. Safe: nothing
-// in that chunk waits for another workgroup.
-template <int MODE = kHandoff, int PF = 3, bool DEFER = false>
+// Workgroups are persistent for at most `max_items` items (round 6, measured against one persistent
+// workgroup per CU): a per-conv launch's short-lived workgroups let the other lane's kernels onto the CUs
+// every ~70 us, and a tower whose 256 workgroups held every CU for the whole forward locked the other lane
+// out (lanes then ran their towers one after another: 6.94M against 7.03M sims/s, configs[1] 17.0M against
+// 25.2M). A workgroup that has run max_items items exits, so CUs free up continuously and out of phase;
+// the grid covers max_items x workgroups >= every item; a workgroup that finds every ticket taken (one sc1
+// load of the ticket, no atomic) exits at once.
+// Counters: two blocks of kTowerCtlWords words used by alternate launches (`parity`), so a late
+// workgroup of this launch that still reads this block's ticket never sees it reset: the workgroup that
+// finishes the launch's last item (items-done counter, [32]) resets the OTHER block (ticket [0], items
+// [32], done[g] [64 + g]) for the next launch and clears max row 0.
+template <int MODE = kHandoff, int PF = 3>
 __global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_stride, const uint16_t *__restrict__ u_all,
                                                      const float *__restrict__ u_scale_all,
                                                      const float *__restrict__ bias_all, int n_layers,
                                                      const uint32_t *__restrict__ stem_amax, uint32_t *rows,
-                                                     int row_stride, uint32_t *ctl, int max_boards,
-                                                     const int32_t *__restrict__ n_dev) {
+                                                     int row_stride, uint32_t *ctl_base, int ctl_words, int parity,
+                                                     int max_items, int max_boards, const int32_t *__restrict__ n_dev) {
     static_assert(MODE & kHandoff, "the tower's hand-offs need the sc1 forms");
     __shared__ __attribute__((aligned(16))) char smem[XP * KC * 4 + VB];
     __shared__ uint32_t s_bmax[SB];
@@ -986,10 +991,18 @@ __global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_str
     float *const sX = reinterpret_cast<float *>(smem);
     char *const sV = smem + XP * KC * 4;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t *const ctl = ctl_base + (size_t)(parity & 1) * ctl_words;
     uint32_t *const done = ctl + kTowerCtlDone;
     int n_boards = max_boards;
     if (n_dev) n_boards = min(n_boards, *n_dev);
     const int nsets = n_sets(n_boards), total = n_layers * nsets;
+    if (total == 0) {  // no item, so no last item: workgroup 0 resets the other block for the next launch
+        if (blockIdx.x == 0) {
+            uint32_t *const other = ctl_base + (size_t)((parity + 1) & 1) * ctl_words;
+            for (int w = tid; w < ctl_words; w += NT) other[w] = 0u;
+        }
+        return;
+    }
     constexpr int UL = NP * C * C * 2;  // u16 per layer
     const int kq = lane >> 4;
     const int voff = wv * 1024 + lane * 16;
@@ -1014,6 +1027,8 @@ __global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_str
     // the sets of group g (2, or 1 for a last group of <= 3 boards)
     auto sets_in = [&](int g) { return min(2, nsets - 2 * g); };
 
+    // a ticket, or `total` once they are all taken (a workgroup that finds none takes nothing)
+    if (tid == 0) s_next[0] = ld_sc1(ctl) >= (uint32_t)total ? total : (int)atomicAdd(ctl, 1u);
     if (tid < SB) s_bmax[tid] = 0u;
     for (int i = fresh(tid); i < NPAD * (KC / 4); i += NT) {  // the staged layout's zero pads (never rewritten)
         const int j = i / (KC / 4), q = i % (KC / 4);
@@ -1028,18 +1043,20 @@ __global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_str
         for (int j = 0; j < 4; ++j) S[i].p[j] = floatx2{0.0f, 0.0f};
     float4 xr[XPT];
     BFrag bq[PF];
-    if (tid == 0) s_next[0] = (int)atomicAdd(ctl, 1u);
     __syncthreads();
     int cur = uni(s_next[0]);
     bool staged = false;  // the current item's first chunk is already staged in sX (and bq holds its U)
     SetScale sc;
     uint32_t nxt_raw = 0u;  // lane 0: the next ticket
-    int pending = -1;       // DEFER: the group whose done signal is still owed (uniform)
+    int items = 0;
+    bool last = false;  // this workgroup finished the launch's last item
 #pragma unroll 1
     while (cur < total) {
         const int l = cur / nsets, st = cur - l * nsets, grp = st >> 1, h = st & 1, b0 = GB * grp + 3 * h;
         const rsrc_t ur = urs(l);
-        if (tid == 0) nxt_raw = atomicAdd(ctl, 1u);  // returns during this item
+        ++items;
+        // the next ticket (returns during this item), unless this is the workgroup's last item
+        if (tid == 0) nxt_raw = items < max_items ? atomicAdd(ctl, 1u) : (uint32_t)total;
         if (!staged) {
             // wait for layer l-1 of this group (one lane polls; the rest join at the barrier), then stage
             if (tid == 0 && l > 0) {
@@ -1084,13 +1101,12 @@ __global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_str
                     const int tl = t / nsets, tg = (t - tl * nsets) >> 1;
                     ready = tl == 0 || ld_sc1(done + tg) >= (uint32_t)(tl * sets_in(tg));
                 }
-                s_next[0] = t;
+                s_next[0] = t < total ? t : total;
                 s_next[1] = ready;
             }
             transform<true, false>(sV, sX, fresh(tid), h);
             lds_barrier();
             if (c + 1 < NCH || nready) store_x(sX, xr, sc_next, fresh(tid));
-            if (DEFER && c == 0 && pending >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             {
                 AFrag a0 = load_a(sv_lane, 0), an;
                 floatx2 mprev[4];
@@ -1104,34 +1120,28 @@ __global__ __launch_bounds__(NT) void k_wino3t_tower(float *act, int64_t act_str
             }
             sc = sc_next;
             lds_barrier();
-            if (DEFER && c == 0 && pending >= 0) {  // the previous item's signal (every wave drained above)
-                if (tid == 0) __hip_atomic_fetch_add(done + pending, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                pending = -1;
-            }
         }
         flush_bmax(s_bmax, rows + (size_t)(l & 3) * row_stride, b0, n_boards, tid);
+        // publish: every wave's stores (outputs, maxima, the cleared row) complete, then one agent-scope add
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(done + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the launch's last item: every other item has published (its add came first)
+            s_next[1] = __hip_atomic_fetch_add(ctl + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (uint32_t)(total - 1);
+        }
+        __syncthreads();
+        last = uni(s_next[1]) != 0;  // (then no ticket is left, so this is also the workgroup's last item)
         cur = nxt;
         staged = nready && nxt < total;
-        if (DEFER && staged) {
-            pending = grp;  // signalled during the next item's first chunk
-        } else {
-            // publish: every wave's stores (outputs, maxima, the cleared row) complete, then one agent-scope add
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_fetch_add(done + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
-    // exit: the last workgroup out resets the counters and clears max row 0 for the next launch
-    if (tid == 0) s_next[0] = (int)(atomicAdd(ctl + 32, 1u) == gridDim.x - 1);
-    __syncthreads();
-    if (s_next[0]) {
-        const int ngroups = (n_boards + GB - 1) / GB;
-        for (int g = tid; g < ngroups; g += NT) done[g] = 0u;
+    if (last) {
+        // reset the other block for the next launch (its launch, the previous one, is complete) and clear max
+        // row 0 (written by conv 28, read by conv 29: both done) for the next forward's conv 0
+        uint32_t *const other = ctl_base + (size_t)((parity + 1) & 1) * ctl_words;
+        for (int w = tid; w < ctl_words; w += NT) other[w] = 0u;
         for (int b = tid; b < row_stride; b += NT) rows[b] = 0u;
-        if (tid == 0) {
-            ctl[0] = 0u;
-            ctl[32] = 0u;
-        }
     }
 }
 

@@ -115,7 +115,8 @@ SIGNATURES = {
                                                   _P]),
     "uttt_nn_conv3x3_wino3h_f16_dev": (ctypes.c_int, [_P, _P, ctypes.c_float, _P, _P, _P, _P, _I32, _P, _P, _I32, _P,
                                                       _I32, _P]),
-    "uttt_nn_tower_wino3h_dev": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I32, _P, _P, _I32, _P, _P, _I32, _P]),
+    "uttt_nn_tower_wino3h_dev": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I32, _P, _P, _I32, _P, _I32, _P, _I32, _P]),
+    "uttt_nn_tower_ctl_words": (ctypes.c_int32, [_I32]),
     "uttt_nn_amax": (ctypes.c_int, [_P, _I64, _P, _P]),
     "uttt_nn_wino3h_set_split": (ctypes.c_int, [_I32]),
 }

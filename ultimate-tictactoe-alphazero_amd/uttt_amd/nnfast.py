@@ -113,10 +113,12 @@ class FusedNetworkEvaluator:
     (uttt_nn_conv3x3_wino3h_f16: one f16 product per point, ~1e-3 relative: the optional fast
     evaluator, not the reference's numerics); None reads UTTT_NN_PRECISION (default f32).
 
-    tower: "dataflow" (default for f32) runs the 32 tower convs as ONE persistent launch
-    (uttt_nn_tower_wino3h_dev: work items (conv, set) handed out in conv-major order, each waiting only
-    for its own board group's previous conv); "layers" launches the convs one by one. Same output bits.
-    None reads UTTT_NN_TOWER."""
+    tower: "layers" (default) launches the 32 tower convs one by one; "dataflow" runs them as ONE persistent
+    launch (uttt_nn_tower_wino3h_dev: work items (conv, set) handed out in conv-major order, each waiting
+    only for its own board group's previous conv; split-f16 only). Same output bits. The dataflow launch is
+    1.2-1.3x faster alone on the GPU at 1.4k-2.7k boards, but holds every CU for the whole forward, so two
+    lanes' towers run one after the other instead of interleaving; in the two-lane headline it is no
+    faster. None reads UTTT_NN_TOWER."""
     needs_input = False
     device_count = True
     NROW = 4  # per-board max rows, rotated over the 32 convs (see __init__, _tower_heads)
@@ -151,7 +153,7 @@ class FusedNetworkEvaluator:
         w = _prepared_weights(net, dev, conv)
         self.stem_w, self.stem_b, self.heads, self.wino = w["stem_w"], w["stem_b"], w["heads"], w["wino"]
         self.u_all, self.bias_all, self.scale_all = w["u_all"], w["bias_all"], w["scale_all"]
-        self.tower = tower or os.environ.get("UTTT_NN_TOWER", "dataflow")
+        self.tower = tower or os.environ.get("UTTT_NN_TOWER", "layers")
         if self.tower not in ("dataflow", "layers"):
             raise ValueError("tower must be 'dataflow' (one persistent launch) or 'layers' (a launch per conv)")
         if self.precision == "f16":
@@ -159,8 +161,10 @@ class FusedNetworkEvaluator:
         # X_even, t, X_odd of the tower as one allocation (the dataflow kernel addresses them by offset)
         self.act = torch.zeros((3, self.max_batch, 81, 128), dtype=torch.float32, device=dev)
         self.buf = [self.act[0], self.act[1], self.act[2]]
-        # the dataflow launch's counters (ticket, exits, done per 7-board group); zero between launches
-        self.ctl = torch.zeros(64 + (self.max_batch + 6) // 7 + 64, dtype=torch.int32, device=dev)
+        # the dataflow launches' counters: two blocks (ticket, items done, done per 7-board group) used by
+        # alternate launches, each launch resetting the other block
+        self.ctl = torch.zeros(2 * self.lib.uttt_nn_tower_ctl_words(self.max_batch), dtype=torch.int32, device=dev)
+        self.ctl_parity = 0
         # The stem's output is bounded for every board by relu(b + sum of the positive weight
         # rows) (its inputs are 0/1 planes): one scale for all boards. Conv i then reads the
         # per-board maxima of its input from row (i-1) % 4, atomically maxes its own output
@@ -231,8 +235,9 @@ class FusedNetworkEvaluator:
     def _tower_dataflow(self, stream, n_dev, max_boards):
         check(self.lib.uttt_nn_tower_wino3h_dev(_p(self.act), ctypes.c_int64(self.act[0].numel()), _p(self.u_all),
                                                 _p(self.scale_all), _p(self.bias_all), self.nconv, _p(self.stem_amax),
-                                                _p(self.bamax), self.max_batch, _p(self.ctl), n_dev, int(max_boards),
-                                                stream))
+                                                _p(self.bamax), self.max_batch, _p(self.ctl), self.ctl_parity, n_dev,
+                                                int(max_boards), stream))
+        self.ctl_parity ^= 1
 
     def _tower_heads(self, n, softmax, n_dev=None):
         stream = self._stream()
