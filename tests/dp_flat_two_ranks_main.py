@@ -31,8 +31,8 @@ if __name__ == "__main__":
 
     # The graphed step over 10 steps at world size 2 against a single-process emulation of the same
     # job: per step, each rank's slice forward in train mode (BatchNorm over that slice
-    # alone), share x its loss backward, the gradients summed, one Adam step. Adam with eps = 1 (updates
-    # ~lr * m_hat, no sign amplification), calibrated network; bounds as tests/rccl_one_rank_main.py (train-mode
+    # alone), share x its loss backward, the gradients summed, one Adam step. Adam with eps = 1e3, lr 10
+    # (updates ~1e-2 m_hat, linear in the gradient: no sign amplification), calibrated network; bounds as tests/rccl_one_rank_main.py (train-mode
     # BatchNorm over 16 samples per rank amplifies rounding): 5% of the weights' motion, 10% of each step's update.
     from uttt_amd.model import calibrated_network
     from uttt_amd.train import DPGraphedStep, local_slice, policy_loss_fn
@@ -43,12 +43,12 @@ if __name__ == "__main__":
     P = torch.softmax(torch.randn(64, 81, generator=g), 1).to(dev)
     V = (torch.rand(64, 1, generator=g) * 2 - 1).to(dev)
     net = calibrated_network(netcal, dev).train()
-    opt = torch.optim.Adam(net.parameters(), lr=torch.tensor(1e-2, device=dev), eps=1.0, capturable=True, fused=True)
+    opt = torch.optim.Adam(net.parameters(), lr=torch.tensor(10.0, device=dev), eps=1e3, capturable=True, fused=True)
     full = local_slice(torch.arange(32), rank, world)
     step = DPGraphedStep(net, opt, X, P, V, len(full), len(full) / 32, graph=True, tune=False)
     assert step.graph
     ref = calibrated_network(netcal, dev).train()
-    opt_r = torch.optim.Adam(ref.parameters(), lr=1e-2, eps=1.0)
+    opt_r = torch.optim.Adam(ref.parameters(), lr=10.0, eps=1e3)
     w0 = [q.detach().clone() for q in ref.parameters()]
     prev = [[q.detach().clone() for q in m.parameters()] for m in (net, ref)]
     hist = []

@@ -251,6 +251,10 @@ int uttt_nn_tower_wino3h_dev(float *act, int64_t act_stride, const uint16_t *u_a
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
+        // persistent workgroups (items 0): UTTT_TOWER_CUS of them (default every CU; fewer leave CUs to the
+        // other lane's kernels)
+        const char *g = getenv("UTTT_TOWER_CUS");
+        if (g && *g && atoi(g) > 0 && atoi(g) < cus) cus = atoi(g);
     }
     const int max_items = n_layers * wino3h::n_sets(max_boards);
     int per = items, wgs;
