@@ -175,6 +175,23 @@ int uttt_search_apply_host(uttt_engine_t *eng, const float *policy, int64_t poli
                            int32_t rows);  /* rows: 1 (one result for the leaf's k copies) or k (one per copy,
                                               applied in order: the reference's call pattern) */
 
+/* A one-tree search as ONE resident wave (round 6; replaces the reference's pv_mcts_scores loop,
+ * uttt_mcts.cpp:84-196, as python_bindings.cpp:11-47 drives it, for uttt_cpp.pv_mcts_scores): search1_begin
+ * launches the wave (root expansion included), which descends to the first flush's leaf and hands it over
+ * through fine-grained pinned memory; search1_next waits for it (n_pending 1: *leaf and its copies k) or for
+ * the search's end (n_pending 0; the tree's error status is raised here); search1_apply writes the leaf's
+ * evaluation (one row for the k copies, or k rows in order) and a command the wave polls, and returns
+ * without waiting; search1_scores copies the root's scores (pv_mcts_scores' return value: one-hot at
+ * temperature 0, else boltzman, as uttt_search_scores) the wave stored at the end. No launch, copy or
+ * stream synchronisation per flush; a wave left without a command for 100 ms exits and search1_next
+ * resumes it. Same results as uttt_search_begin + uttt_search_select_host / apply_host + scores. */
+int uttt_search1_begin(uttt_engine_t *eng, const uttt_state_t *root, int32_t sims, int32_t batch, int32_t semantics,
+                       float temperature);
+int uttt_search1_next(uttt_engine_t *eng, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending);
+int uttt_search1_apply(uttt_engine_t *eng, const float *policy, int64_t policy_stride, const float *value,
+                       int32_t rows);
+int uttt_search1_scores(uttt_engine_t *eng, float *scores, int32_t *n_legal);
+
 /* Evaluator results for the pending leaves (uttt_mcts.cpp:138-167: legal-mask,
  * sequential f32 renormalisation, expand k times, back up k times).
  * Row r of policy (>= 81 f32, stride policy_ld) / value (stride value_ld)

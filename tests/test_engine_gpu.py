@@ -385,6 +385,57 @@ def test_uttt_cpp_callback_search_matches_golden(gpu):
     assert len(calls) == d["flushes"][r] and sum(calls) == d["evals"][r]
 
 
+def test_uttt_cpp_resident_search_resumes_and_recovers(gpu):
+    """uttt_cpp.pv_mcts_scores runs the whole search as one resident wave (round 6, uttt_search1_*). A model
+    slower than the wave's 100 ms wait for a command (the wave exits; the next flush resumes it with the
+    command it did not see applied first), and a model that raises mid-search (the wave is left resident;
+    the next search stops it first) both leave the golden scores bit-exact."""
+    import time
+    import uttt_cpp
+    from oracle.hashnp import hash_eval_np
+    d = golden("search.npz")
+    rows = np.nonzero((d["sims"] == 50) & (d["batch"] == 8))[0]
+    r = int(rows[0])
+    i = int(d["pos"][r])
+
+    def state():
+        return uttt_cpp.State(d["pos_pieces"][i].reshape(9, 9).tolist(), d["pos_enemy"][i].reshape(9, 9).tolist(),
+                              d["pos_main_p"][i].tolist(), d["pos_main_e"][i].tolist(), int(d["pos_active"][i]))
+
+    def evaluate(states):
+        out = []
+        for s in states:
+            x = np.asarray(s.to_input_tensor(), np.float32).reshape(9, 9, 3).transpose(2, 0, 1)
+            p, v = hash_eval_np(x)
+            out.append((p, float(v)))
+        return out
+
+    calls = []
+
+    def slow(states):
+        calls.append(len(states))
+        if len(calls) in (2, 4):
+            time.sleep(0.25)
+        return evaluate(states)
+
+    def search(model):
+        return np.asarray(uttt_cpp.pv_mcts_scores(model=model, state=state(), temperature=float(d["temp"][r]),
+                                                  evaluate_count=50, batch_size=8), np.float32)
+
+    n = int(d["n"][r])
+    sc = search(slow)
+    assert np.array_equal(sc.view(np.uint32), d["scores"][r][:n].view(np.uint32))
+    assert len(calls) == d["flushes"][r]
+
+    def failing(states):
+        raise RuntimeError("model failure")
+
+    with pytest.raises(RuntimeError, match="model failure"):
+        search(failing)
+    sc = search(evaluate)
+    assert np.array_equal(sc.view(np.uint32), d["scores"][r][:n].view(np.uint32))
+
+
 def test_network_gpu_matches_cpu_fp32(gpu):
     """Value within 1e-5 of CPU fp32 (north star). The random-init net is saturated
     (|logits| up to ~1e2..1e3), so the policy is checked on its logits, relative to

@@ -1717,6 +1717,150 @@ __global__ void k_root_scores(Pool pool, Trees tr, float temperature, float *sco
     n_legal[t] = L;
 }
 
+// ------------------------------------------------- resident one-tree search --
+// A whole one-tree search as ONE resident wave (round 6; uttt_search1_*): the reference's
+// pv_mcts_scores (uttt_mcts.cpp:84-196) driven through python_bindings.cpp:11-47 calls the model once per
+// flush, so the search needs the host between flushes; instead of a launch per flush (k_flush1), the wave
+// stays resident and meets the host through fine-grained pinned memory (Search1Host): it writes the flush's
+// leaf, its copies and a sequence tag (system-scope release), polls for the host's command (the evaluation
+// rows the host wrote beside it, then the command's sequence), applies them (k_apply's body) and descends
+// to the next leaf (k_select's body); when the tree has no simulation left it computes the root's scores
+// (k_root_scores' body) into host memory and exits. Same tree, same order of operations as k_begin +
+// k_flush1 + k_root_scores, so the same results. Exit conditions every path reaches: the search's end, the
+// host's exit word, and 100 ms without a command (s_memrealtime at 100 MHz); after a timeout the host
+// relaunches the wave in resume mode (the command it wrote is applied first).
+struct Search1Host {
+    // device -> host
+    int32_t tag, count, k, status;  // a leaf (count 1) or the end (count 0); status: the tree's error bits
+    int32_t n_legal, gone, pad0, pad1;  // gone: the command sequence the wave timed out waiting for (0: none)
+    uttt_state_t leaf;
+    float scores[81];
+    // host -> device
+    int32_t cmd_seq, cmd_rows, cmd_exit, pad2;
+    // the evaluation rows: policy [rows][96] (81 used), value [rows], row base 0 (one leaf)
+};
+constexpr int kSearch1Timeout = 10000000;  // 100 ms of s_memrealtime (100 MHz)
+
+template <bool PY>
+__global__ __launch_bounds__(kWave) void k_search1(Pool pool, Trees tr, EvalCache cache, uttt_state_t root,
+                                                   float temperature, Search1Host *hs, const float *policy,
+                                                   const float *value, const int32_t *rowbase, int32_t seq,
+                                                   int32_t resume) {
+    __shared__ __attribute__((aligned(16))) float s_row[84];
+    const int lane = lane_id();
+    if (!resume) {  // k_begin's body for tree 0 (root expanded with uniform priors; py semantics: plain root)
+        uint32_t m[3];
+        legal_mask(root, m);
+        if (tr.py) {
+            const bool any = __ballot(bit_of(m, lane) != 0u) != 0ull || __ballot(lane < 17 && bit_of(m, 64 + lane) != 0u);
+            if (lane == 0) {
+                pool.rec[0] = make_uint4(0u, 0u, make_meta(kNoAction, 0u), 0u);
+                tr.root[0] = root;
+                TreeCtl c;
+                c.sims_done = 0;
+                c.node_count = 1;
+                c.status = any ? kLive : 0;
+                c.pad = 0;
+                tr.ctl[0] = c;
+            }
+        } else {
+            const bool l0 = bit_of(m, lane) != 0u;
+            const bool l1 = lane < 17 && bit_of(m, 64 + lane) != 0u;
+            const uint64_t b0 = __ballot(l0), b1 = __ballot(l1);
+            const int L = __popcll(b0) + __popcll(b1);
+            const float up = L ? 1.0f / (float)L : 0.0f;
+            if (l0) pool.rec[1 + __popcll(b0 & lanes_below())] = new_child(up, (uint32_t)lane);
+            if (l1) pool.rec[1 + __popcll(b0) + __popcll(b1 & lanes_below())] = new_child(up, (uint32_t)(64 + lane));
+            if (lane == 0) {
+                pool.rec[0] = make_uint4(0u, 0u, make_meta(kNoAction, (uint32_t)L), make_link(L ? 1u : 0u, L ? 1u : 0u));
+                tr.root[0] = root;
+                TreeCtl c;
+                c.sims_done = 0;
+                c.node_count = 1 + L;
+                c.status = L > 0 ? kLive : 0;
+                c.pad = 0;
+                tr.ctl[0] = c;
+            }
+        }
+        wave_memory_fence();
+    }
+    bool apply = resume != 0;  // resume: the command of sequence `seq` is waiting in host memory
+    for (;;) {
+        if (apply) {
+            const int rows = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&hs->cmd_rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+            // per-copy rows bypass the evaluation cache (as host_apply_args)
+            EvalCache acache = cache;
+            if (rows > 1) acache.flag = nullptr;
+            apply_wave(pool, tr, acache, policy, 96, value, 1, rowbase, rows > 1 ? 1 : 0, nullptr, 0, s_row, 0,
+                       __builtin_amdgcn_readfirstlane(tr.pending[0]) >> 8);
+            wave_memory_fence();  // the descent reads the records the apply wrote
+        }
+        const int p = select_wave<PY>(pool, tr, cache, nullptr, 0, s_row, nullptr, 0);
+        const int q = p & 0xFF;
+        if (q == 2) {  // stopped by the select budget before a leaf: descend again (as uttt_search_select_host)
+            apply = false;
+            continue;
+        }
+        ++seq;
+        if (q == 1 || q == 3) {  // a leaf: hand it to the host
+            wave_memory_fence();
+            if (lane == 0) {
+                const uttt_state_t lf = tr.leaf[0];
+                const int32_t *w = reinterpret_cast<const int32_t *>(&lf);
+                int32_t *d = reinterpret_cast<int32_t *>(&hs->leaf);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&hs->k, tr.rec[0].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&hs->count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&hs->tag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            // wait for the host's command of this sequence (its rows were written before it)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            int got = 0;
+            for (;;) {
+                int c = 0, x = 0;
+                if (lane == 0) {
+                    c = __hip_atomic_load(&hs->cmd_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    x = __hip_atomic_load(&hs->cmd_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                c = __builtin_amdgcn_readfirstlane(c);
+                x = __builtin_amdgcn_readfirstlane(x);
+                if (c == seq) {
+                    got = 1;
+                    break;
+                }
+                if (x) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)kSearch1Timeout) {
+                    if (lane == 0) __hip_atomic_store(&hs->gone, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!got) return;
+            apply = true;
+            continue;
+        }
+        // the search's end: the root's scores (k_root_scores' body) and the tree's status, then the tag
+        wave_memory_fence();
+        int L = 0;
+        if (lane == 0) root_scores(pool, 0, temperature, s_row, L);  // the LDS row as the working buffer
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        L = __builtin_amdgcn_readfirstlane(L);
+        for (int i = lane; i < 81; i += kWave)
+            __hip_atomic_store(&hs->scores[i], i < L ? s_row[i] : 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) {
+            __hip_atomic_store(&hs->n_legal, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hs->status, (int32_t)(tr.ctl[0].status & kErrMask), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hs->count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&hs->tag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+}
+
 // -------------------------------------------------------------- self-play --
 struct Slot {
     uttt_state_t state;
@@ -2199,6 +2343,12 @@ struct uttt_engine {
     const float *dev_apply_policy = nullptr, *dev_apply_value = nullptr;
     bool dev_apply_staged = false;
     bool dev_apply_by_tree = false;  // staged by a one-dispatch round (k_round1): rows by tree, no scan
+    // the resident one-tree search (uttt_search1_*, k_search1): its host block and evaluation rows
+    Search1Host *h_s1 = nullptr;  // fine-grained pinned: Search1Host, then policy [cap][96], value [cap], row base
+    int32_t s1_cap = 0, s1_seq = 0;
+    bool s1_alive = false;  // a k_search1 wave may still be resident on the stream
+    uttt_state_t s1_root{};
+    float s1_temperature = 0.0f;
     uint32_t *d_r1ctl = nullptr;     // k_round1's arrival counters and per-block partials (zero between rounds)
     int32_t host_apply_rows = 0;  // a one-tree evaluation staged by uttt_search_apply_host, applied by the next
                                   // k_flush1 (or by flush_host_apply before any other call that reads the tree)
@@ -2472,9 +2622,11 @@ int uttt_engine_create(int32_t device, int32_t max_trees, int32_t max_sims, uttt
     return UTTT_OK;
 }
 
+static int search1_stop(uttt_engine *e);
 int uttt_engine_destroy(uttt_engine_t *e) {
     if (!e) return UTTT_OK;
     (void)hipSetDevice(e->device);
+    (void)search1_stop(e);  // a resident one-tree search wave exits first
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     drain_events(e);
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -2490,6 +2642,7 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     if (e->h_ring) (void)hipHostFree(e->h_ring);
     if (e->h_leaf) (void)hipHostFree(e->h_leaf);
     if (e->h_eval) (void)hipHostFree(e->h_eval);
+    if (e->h_s1) (void)hipHostFree(e->h_s1);
     if (e->h_move) (void)hipHostFree(e->h_move);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     delete e;
@@ -2513,7 +2666,9 @@ int uttt_engine_set_stream(uttt_engine_t *e, void *stream) {
 
 int64_t uttt_engine_device_bytes(const uttt_engine_t *e) { return e ? e->bytes : 0; }
 
+static int search1_stop(uttt_engine *e);
 static int search_begin_common(uttt_engine *e, int32_t n_trees, int32_t sims, int32_t batch) {
+    if (int rc0 = search1_stop(e)) return rc0;  // a resident one-tree search left unfinished
     e->dev_apply_staged = false;  // a staged round of a search that was never ended is dropped with it
     e->host_apply_rows = 0;       // (and a staged one-tree evaluation)
     if (n_trees <= 0 || n_trees > e->max_trees) {
@@ -2750,6 +2905,166 @@ static int flush_host_apply(uttt_engine *e) {
     timed_launch(e, kKApply, k_apply, dim3(grid_waves(1)), dim3(kBlock), e->pool, e->tr, a.cache, a.policy,
                  (int64_t)96, a.value, (int64_t)1, a.rowbase, a.per_copy, bytes_ptr(e, kKApply));
     return check_launch();
+}
+
+// ---- the resident one-tree search (k_search1) ----
+static float *s1_policy(uttt_engine *e) { return reinterpret_cast<float *>(e->h_s1 + 1); }
+static float *s1_value(uttt_engine *e) { return s1_policy(e) + (size_t)e->s1_cap * 96; }
+static int32_t *s1_rowbase(uttt_engine *e) { return reinterpret_cast<int32_t *>(s1_value(e) + e->s1_cap); }
+
+// a resident wave left by an unfinished search exits (its exit word) before anything else runs on the stream
+static int search1_stop(uttt_engine *e) {
+    if (!e->s1_alive) return UTTT_OK;
+    __atomic_store_n(&e->h_s1->cmd_exit, 1, __ATOMIC_SEQ_CST);
+    e->s1_alive = false;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return UTTT_OK;
+}
+
+static int search1_launch(uttt_engine *e, int32_t resume) {
+    hipLaunchKernelGGL(e->tr.py ? k_search1<true> : k_search1<false>, dim3(1), dim3(kWave), 0, e->stream, e->pool, e->tr,
+                       e->cache, e->s1_root, e->s1_temperature, e->h_s1, (const float *)s1_policy(e),
+                       (const float *)s1_value(e), (const int32_t *)s1_rowbase(e), e->s1_seq, resume);
+    e->s1_alive = true;
+    return check_launch();
+}
+
+int uttt_search1_begin(uttt_engine_t *e, const uttt_state_t *root, int32_t sims, int32_t batch, int32_t semantics,
+                       float temperature) {
+    if (!e || !root || (semantics != UTTT_SEMANTICS_CPP && semantics != UTTT_SEMANTICS_PY)) {
+        set_error("uttt_search1_begin: bad arguments (semantics 0 = cpp, 1 = py)");
+        return UTTT_ERR_ARG;
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    if (int rc0 = search1_stop(e)) return rc0;
+    int rc = search_begin_common(e, 1, sims, batch);
+    if (rc) return rc;
+    e->tr.py = semantics == UTTT_SEMANTICS_PY ? 1 : 0;
+    e->selfplay = false;
+    const int32_t need = e->tr.batch > 16 ? e->tr.batch : 16;  // rows per flush: 1 or k <= batch
+    if (need > e->s1_cap) {
+        if (e->h_s1) (void)hipHostFree(e->h_s1);  // no wave is resident (search1_stop)
+        e->h_s1 = nullptr;
+        e->s1_cap = 0;
+        const size_t bytes = sizeof(Search1Host) + (size_t)need * 97 * sizeof(float) + 16;
+        if (hipHostMalloc((void **)&e->h_s1, bytes, hipHostMallocCoherent) != hipSuccess) {
+            set_error("hipHostMalloc failed");
+            return UTTT_ERR_HIP;
+        }
+        memset((void *)e->h_s1, 0, bytes);
+        e->s1_cap = need;
+    }
+    Search1Host *h = e->h_s1;
+    h->tag = 0;
+    h->gone = 0;
+    h->cmd_seq = 0;
+    h->cmd_exit = 0;
+    h->count = 0;
+    s1_rowbase(e)[0] = 0;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    e->s1_root = *root;
+    e->s1_temperature = temperature;
+    e->s1_seq = 0;
+    e->phase = 1;
+    e->n_pending = 0;
+    return search1_launch(e, 0);
+}
+
+int uttt_search1_next(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending) {
+    if (!e || !leaf || !copies || !n_pending) return UTTT_ERR_ARG;
+    if (e->phase != 1 || !e->h_s1 || !e->s1_alive) {
+        set_error("uttt_search1_next: call uttt_search1_begin (or apply the previous leaf) first");
+        return UTTT_ERR_ORDER;
+    }
+    const int32_t want = e->s1_seq + 1;
+    Search1Host *h = e->h_s1;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(&h->tag, __ATOMIC_ACQUIRE) == want) break;
+        if ((it & 255u) == 0u) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                set_error("engine stream failed: %s", hipGetErrorString(q));
+                return UTTT_ERR_HIP;
+            }
+            if (q == hipSuccess && __atomic_load_n(&h->tag, __ATOMIC_ACQUIRE) != want) {
+                // the wave timed out waiting for the previous command (the host took over 100 ms): resume it,
+                // the command it did not see applied first
+                if (__atomic_load_n(&h->gone, __ATOMIC_ACQUIRE) != e->s1_seq || e->s1_seq == 0) {
+                    set_error("engine: the resident search left without storing its result");
+                    return UTTT_ERR_HIP;
+                }
+                h->gone = 0;
+                __atomic_thread_fence(__ATOMIC_SEQ_CST);
+                if (int rc0 = search1_launch(e, 1)) return rc0;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                set_error("engine: one-tree search result not stored within 60 s");
+                return UTTT_ERR_HIP;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    e->s1_seq = want;
+    const int n = __atomic_load_n(&h->count, __ATOMIC_ACQUIRE);
+    if (n > 0) {
+        memcpy(leaf, const_cast<const uttt_state_t *>(&h->leaf), sizeof(uttt_state_t));
+        *copies = h->k;
+        e->n_pending = 1;
+        e->phase = 2;
+    } else {
+        e->s1_alive = false;  // the wave ends after the search's end
+        e->n_pending = 0;
+        e->phase = 1;
+        const uint32_t st = (uint32_t)__atomic_load_n(&h->status, __ATOMIC_ACQUIRE);
+        if (st & kErrMask) {
+            set_error("tree 0 failed (status 0x%x: %s)", st, tree_error_text(st));
+            return tree_error_code(st);
+        }
+    }
+    *n_pending = n;
+    return UTTT_OK;
+}
+
+int uttt_search1_apply(uttt_engine_t *e, const float *policy, int64_t pld, const float *value, int32_t rows) {
+    if (!e || !policy || !value || pld < 81 || rows < 1) {
+        set_error("uttt_search1_apply: bad arguments (policy stride must be >= 81, rows >= 1)");
+        return UTTT_ERR_ARG;
+    }
+    if (e->phase != 2 || !e->s1_alive) {
+        set_error("uttt_search1_apply: no pending leaf (call uttt_search1_next)");
+        return UTTT_ERR_ORDER;
+    }
+    Search1Host *h = e->h_s1;
+    const int32_t k = h->k;
+    if ((rows != 1 && rows != k) || rows > e->s1_cap) {
+        set_error("uttt_search1_apply: %d results for a leaf queued %d times (pass 1 or %d)", rows, k, k);
+        return UTTT_ERR_ARG;
+    }
+    float *hp = s1_policy(e), *hv = s1_value(e);
+    for (int32_t r = 0; r < rows; ++r) {
+        memcpy(hp + (size_t)r * 96, policy + (size_t)r * pld, 81 * sizeof(float));
+        hv[r] = value[r];
+    }
+    __atomic_store_n(&h->cmd_rows, rows, __ATOMIC_RELAXED);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // the rows before the command the wave polls
+    __atomic_store_n(&h->cmd_seq, e->s1_seq, __ATOMIC_RELEASE);
+    e->phase = 1;
+    e->n_pending = 0;
+    return UTTT_OK;
+}
+
+int uttt_search1_scores(uttt_engine_t *e, float *scores, int32_t *n_legal) {
+    if (!e || !scores || !n_legal) return UTTT_ERR_ARG;
+    if (!e->h_s1 || e->s1_alive || e->phase != 1) {
+        set_error("uttt_search1_scores: the search has not ended (uttt_search1_next returns no leaf at its end)");
+        return UTTT_ERR_ORDER;
+    }
+    const Search1Host *h = e->h_s1;
+    const int L = h->n_legal;
+    for (int i = 0; i < 81; ++i) scores[i] = i < L ? h->scores[i] : 0.0f;
+    *n_legal = L;
+    return UTTT_OK;
 }
 
 int uttt_search_select_host(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copies, int32_t *n_pending) {

@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -125,7 +126,14 @@ py::list pv_mcts_scores(py::object model, const State &state, float temperature,
         return py::cast(out);
     }
     uttt_engine_t *eng = search_engine().get(evaluate_count);
-    check(uttt_search_begin(eng, &state.s, 1, evaluate_count, batch_size));
+    // round 6: the whole search as one resident wave (uttt_search1_*: no launch per flush, the scores
+    // stored by the wave at the end); UTTT_SEARCH1=0 keeps the launch per flush of round 5
+    static const bool resident = [] {
+        const char *v = getenv("UTTT_SEARCH1");
+        return !(v && v[0] == '0');
+    }();
+    if (resident) check(uttt_search1_begin(eng, &state.s, evaluate_count, batch_size, UTTT_SEMANTICS_CPP, temperature));
+    else check(uttt_search_begin(eng, &state.s, 1, evaluate_count, batch_size));
     // per flush: the round's leaf and its copies k come back through pinned host memory the scan writes
     // (uttt_search_select_host), the results go to pinned memory k_apply reads (uttt_search_apply_host): no
     // copy operation and no stream synchronisation per flush besides the model's own
@@ -133,7 +141,8 @@ py::list pv_mcts_scores(py::object model, const State &state, float temperature,
     for (;;) {
         int32_t n = 0, k = 0;
         uttt_state_t leaf;
-        check(uttt_search_select_host(eng, &leaf, &k, &n));
+        if (resident) check(uttt_search1_next(eng, &leaf, &k, &n));
+        else check(uttt_search_select_host(eng, &leaf, &k, &n));
         if (n == 0) break;
         const int copies = dedup ? 1 : k;
         py::list batch;
@@ -150,11 +159,13 @@ py::list pv_mcts_scores(py::object model, const State &state, float temperature,
         if (got < copies)
             throw std::runtime_error("model returned " + std::to_string(got) + " results for " + std::to_string(copies) +
                                      " states");
-        check(uttt_search_apply_host(eng, pol.data(), 81, val.data(), copies));
+        if (resident) check(uttt_search1_apply(eng, pol.data(), 81, val.data(), copies));
+        else check(uttt_search_apply_host(eng, pol.data(), 81, val.data(), copies));
     }
     float scores[81];
     int32_t L = 0;
-    check(uttt_search_scores(eng, temperature, scores, &L));
+    if (resident) check(uttt_search1_scores(eng, scores, &L));
+    else check(uttt_search_scores(eng, temperature, scores, &L));
     return py::cast(std::vector<float>(scores, scores + L));
 }
 
