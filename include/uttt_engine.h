@@ -220,6 +220,11 @@ int uttt_eval_hash_dev(uttt_engine_t *eng, float *policy, float *value);
  * has run. Replaces, for the test evaluator, one pass of the flush loop of uttt_mcts.cpp:109-167
  * over every tree. */
 int uttt_round_hash_async(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, float *policy, float *value);
+/* n_rounds consecutive rounds in one call (round 6, tree-only self-play: the host's per-round reaction was
+ * the bound): ring slots ring_slot .. ring_slot + n_rounds - 1 (mod 8) and tags tag .. tag + n_rounds - 1;
+ * a round past the move's last finds every tree done and changes nothing. */
+int uttt_rounds_hash_async(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, float *policy, float *value,
+                           int32_t n_rounds);
 
 /* Root results after the search: visit counts of the root's children (legal
  * order, row stride 81) and |legal| per tree. */

@@ -73,24 +73,23 @@ if __name__ == "__main__":
         err = (qa.grad - qb.grad).abs().max().item()
         assert err <= 1e-3 * scale, (k, err, scale)
 
-    # Graph replays against the same phases run eagerly, over 12 steps. Adam with
-    # eps = 1e3 and lr 10 makes each update ~1e-2 m_hat, linear in the gradient while |g| << 1e3 (eps = 1 was
-    # not: the large gradients of this net made sqrt(v_hat) >> eps again), so rounding-level differences between
-    # the kernels MIOpen picks inside and outside a capture stay rounding-level instead of flipping
-    # lr * sign(g) updates; the calibrated (non-saturated) network; a new random slice every step (the
-    # index copy into the graph's input); the learning-rate tensor changed at step 6 (read by the replay);
-    # Adam's step counter and bias correction advance inside graph B. A replay bug (a stale flat gradient,
-    # a stale lr or step, the warm-up undo leaving state behind) moves the graph's weights by O(update)
-    # from the eager ones. Train-mode BatchNorm over 16 samples amplifies rounding: graph and eager
-    # gradients differ by ~0.1-1% of their scale (a CPU run of the same loss moves by 2e-4 to 2e-2 of it with
-    # the host thread count alone), so the checks bound (a) the distance at 5% of how far the weights moved
-    # and (b) each step's update difference at 10% of that update; a stale lr (x3.3 at step 6), step counter
-    # or gradient breaks (b) by an O(1) factor.
+    # Graph replays against the same phases run eagerly, over 12 steps: a new random
+    # slice every step (the index copy into the graph's input), the learning-rate tensor changed at step 6
+    # (read by the replay), Adam's step counter and bias correction advancing inside graph B. A replay bug (a
+    # stale flat gradient, a stale lr or step, the warm-up undo leaving state behind) moves the graph's weights
+    # by O(update) from the eager ones. The comparison is made well-conditioned on purpose: BatchNorm in eval
+    # mode (the calibrated running statistics; in train mode a channel with near-zero batch variance over 16
+    # samples multiplies rounding by up to 1/sqrt(eps) = 316, and the graph and eager runs, whose MIOpen
+    # kernels differ in rounding, part by 10% of an update within 4 steps), and Adam with eps = 1e3 and lr 10,
+    # so each update is ~1e-2 m_hat, linear in the gradient (no lr * sign(g) amplification). Bounds: the
+    # distance at 1% of how far the weights moved, each step's update difference at 2% of that update; a
+    # stale lr (x3.3 at step 6), step counter or gradient breaks the second by an O(1) factor. (Train mode,
+    # the per-rank BatchNorm path, is pinned at step 1 above and in tests/dp_flat_two_ranks_main.py.)
     from uttt_amd.model import calibrated_network
     netcal = os.path.join(REPO, "tests", "golden", "netcal.npz")
     nets, steps, lrs = [], [], []
     for graph in (True, False):
-        net = calibrated_network(netcal, "cuda").train()
+        net = calibrated_network(netcal, "cuda").eval()
         lr_t = torch.tensor(10.0, device="cuda")
         opt = torch.optim.Adam(net.parameters(), lr=lr_t, eps=1e3, capturable=True, fused=True)
         nets.append(net)
@@ -110,8 +109,7 @@ if __name__ == "__main__":
             st.loss_sum.zero_()
             st.step(idx, 1.0)
         lg, le = float(steps[0].loss_sum), float(steps[1].loss_sum)
-        # (the loss follows the weights' rounding-level drift: 1.2e-4 apart by step 4 on one box)
-        assert np.isfinite(lg) and abs(lg - le) <= 2e-3 * abs(le), (t, lg, le, hist)
+        assert np.isfinite(lg) and abs(lg - le) <= 1e-4 * abs(le), (t, lg, le, hist)
         moved = max((qe.detach() - q0).abs().max().item() for qe, q0 in zip(nets[1].parameters(), w0))
         diff = max((qg.detach() - qe.detach()).abs().max().item()
                    for qg, qe in zip(nets[0].parameters(), nets[1].parameters()))
@@ -120,7 +118,7 @@ if __name__ == "__main__":
         step_e = max(d.abs().max().item() for d in inc[1])
         step_d = max((a - b).abs().max().item() for a, b in zip(inc[0], inc[1]))
         prev = [[q.detach().clone() for q in n.parameters()] for n in nets]
-        assert diff <= 5e-2 * moved and step_d <= 0.1 * step_e, (t, diff, moved, step_d, step_e, hist)
+        assert diff <= 1e-2 * moved and step_d <= 2e-2 * step_e, (t, diff, moved, step_d, step_e, hist)
         hist.append((round(lg, 6), round(le, 6), round(diff / moved, 5), round(step_d / step_e, 5)))
     dist.destroy_process_group()
     print("RCCL-OK", losses, "flat-graph DP", la, "eager DDP", lb, flush=True)

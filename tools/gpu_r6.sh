@@ -40,11 +40,15 @@ for s in $STEPS; do
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated --evaluator hash --lanes 1 --age 100 \
                --steps 20 --warmup 3 > $OUT/tprof_bench.log 2>&1 && \
            python3 tools/prof_summary.py $(ls $OUT/tprof/*/bench_kernel_trace.csv $OUT/tprof/bench_kernel_trace.csv 2>/dev/null | head -1) \
-               $OUT/tprof_bench.log $OUT/prof_tree_only.md > $OUT/tprof_summary.log 2>&1 ;;
+               $OUT/tprof_bench.log $OUT/prof_tree_only.md > $OUT/tprof_summary.log 2>&1 && \
+           { cp $(ls $OUT/tprof/*/bench_kernel_stats.csv $OUT/tprof/bench_kernel_stats.csv 2>/dev/null | head -1) \
+               $OUT/tprof_kernel_stats.csv 2>/dev/null; rm -rf $OUT/tprof; true; } ;;
     hprof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/hprof -o bench \
                -- python3 bench.py --no-cpu-baseline --no-variants --no-isolated ${BENCH_ARGS:-} > $OUT/hprof_bench.log 2>&1 && \
            python3 tools/prof_summary.py $(ls $OUT/hprof/*/bench_kernel_trace.csv $OUT/hprof/bench_kernel_trace.csv 2>/dev/null | head -1) \
-               $OUT/hprof_bench.log $OUT/prof_headline.md > $OUT/hprof_summary.log 2>&1 ;;
+               $OUT/hprof_bench.log $OUT/prof_headline.md > $OUT/hprof_summary.log 2>&1 && \
+           { cp $(ls $OUT/hprof/*/bench_kernel_stats.csv $OUT/hprof/bench_kernel_stats.csv 2>/dev/null | head -1) \
+               $OUT/hprof_kernel_stats.csv 2>/dev/null; rm -rf $OUT/hprof; true; } ;;
     pmctree) UTTT_FUSED_ROUNDS=0 PMC_OUT=$OUT/pmc_tree PMC_AGE=100 PMC_BENCH_ARGS="--evaluator hash --lanes 1" timeout -k 10 900 bash tools/pmc_select.sh \
                > $OUT/pmc_tree.log 2>&1 && \
              python tools/pmc_summary.py $OUT/pmc_tree $OUT/pmc_tree/p1.log $OUT/pmc_select_tree.json k_select >> $OUT/pmc_tree.log && \

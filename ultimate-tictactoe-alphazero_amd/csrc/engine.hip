@@ -3244,6 +3244,19 @@ static int select_async_then_stage(uttt_engine *e, int32_t ring_slot, int32_t ta
     return UTTT_OK;
 }
 
+int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value);
+
+int uttt_rounds_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value,
+                           int32_t n_rounds) {
+    if (!e || n_rounds < 1 || n_rounds > kCountRing) {
+        set_error("uttt_rounds_hash_async: n_rounds must be in 1..%d", kCountRing);
+        return UTTT_ERR_ARG;
+    }
+    for (int32_t i = 0; i < n_rounds; ++i)
+        if (int rc = uttt_round_hash_async(e, (ring_slot + i) % kCountRing, tag + i, policy, value)) return rc;
+    return UTTT_OK;
+}
+
 int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value) {
     if (!e || !policy || !value || ring_slot < 0 || ring_slot >= kCountRing) {
         set_error("uttt_round_hash_async: bad arguments (ring slot must be in 0..%d)", kCountRing - 1);

@@ -188,6 +188,16 @@ class Engine:
         check(self.lib.uttt_eval_hash_dev(self.h, ctypes.c_void_p(policy.data_ptr()),
                                           ctypes.c_void_p(value.data_ptr())))
 
+    def rounds_hash_async(self, ring_slot, policy, value, n_rounds):
+        """n_rounds consecutive hash rounds in one call (uttt_rounds_hash_async): ring slots ring_slot ..
+        ring_slot + n_rounds - 1 (mod 8), tags tag + 1 .. tag + n_rounds; returns the last round's tag."""
+        first = self._next_tag()
+        self.tag = (first + n_rounds - 1) & 0x7FFFFFFF
+        check(self.lib.uttt_rounds_hash_async(self.h, int(ring_slot), first, ctypes.c_void_p(policy.data_ptr()),
+                                              ctypes.c_void_p(value.data_ptr()), int(n_rounds)))
+        self.n_pending = None
+        return self.tag
+
     def round_hash_async(self, ring_slot, policy, value):
         """A whole round with the hash evaluator in one call (uttt_round_hash_async): select, scan (the counts
         and then a new tag into ring slot ring_slot), hash evaluation of the pending leaves, apply. Returns

@@ -34,12 +34,6 @@ class HashEvaluator:
     device_count = True
     cheap = True  # SelfPlay keeps two rounds in flight: the host's reaction, not the kernels, set the pace
 
-    def __init__(self, engine):
-        self.engine = engine
-        dev = torch.device("cuda", engine.device)
-        self.policy = torch.zeros((engine.max_trees, 81), dtype=torch.float32, device=dev)
-        self.value = torch.zeros((engine.max_trees, 1), dtype=torch.float32, device=dev)
-
     def __call__(self, x, n):
         if isinstance(n, RoundCount):
             self.engine.eval_hash_dev(self.policy, self.value)
@@ -47,11 +41,24 @@ class HashEvaluator:
         self.engine.eval_hash(x, n, self.policy, self.value)
         return self.policy[:n], self.value[:n]
 
+    def __init__(self, engine):
+        self.engine = engine
+        dev = torch.device("cuda", engine.device)
+        self.policy = torch.zeros((engine.max_trees, 81), dtype=torch.float32, device=dev)
+        self.value = torch.zeros((engine.max_trees, 1), dtype=torch.float32, device=dev)
+        # rounds per C call (round 6): each call enqueues this many one-dispatch rounds and the host polls only
+        # the last one's tag, so the host's per-round reaction (the tree-only bound) is paid once per call;
+        # rounds past the move's end find every tree done. UTTT_ROUND_BATCH (1 = one round per call).
+        self.rounds_per_call = max(1, min(4, int(os.environ.get("UTTT_ROUND_BATCH", "4"))))
+
     def round_async(self, engine, slot):
-        """The whole round in one C call (Engine.round_hash_async: the previous round's apply and this round's
-        select as one k_round launch, scan, this evaluator; this round's apply is staged for the next call or
-        the move's end). SelfPlay.steps then polls the returned tag in the host count ring instead of an event."""
-        return engine.round_hash_async(slot, self.policy, self.value)
+        """rounds_per_call whole rounds in one C call (Engine.rounds_hash_async: per round one k_round1 launch
+        that applies the previous round's evaluation, descends, evaluates the new leaves and publishes the
+        counts; the last round's apply is staged for the next call or the move's end). SelfPlay.steps then
+        polls the last round's tag in the host count ring instead of an event."""
+        if self.rounds_per_call == 1:
+            return engine.round_hash_async(slot, self.policy, self.value)
+        return engine.rounds_hash_async(slot, self.policy, self.value, self.rounds_per_call)
 
 
 class NetworkEvaluator:
@@ -316,8 +323,9 @@ class SelfPlay:
         for ln in self.lanes:
             if ln.count_ring is None:
                 ln.count_ring = ln.engine.count_ring()  # the scan writes each round's counts here
-            if len(ln.count_ring) < depth + 1:
-                raise ValueError(f"round look-ahead {depth} needs {depth + 1} count slots")
+            r = getattr(ln.evaluator, "rounds_per_call", 1)
+            if len(ln.count_ring) < (depth + 1) * r and not (r > 1 and len(ln.count_ring) >= depth * r):
+                raise ValueError(f"round look-ahead {depth} x {r} rounds per call needs more count slots")
 
         def fill(ln, q):
             # rounds in flight per lane: one (the next is enqueued once this one's count is read), or,
@@ -352,7 +360,10 @@ class SelfPlay:
                     ln.result_pending = False
                     if progress:
                         progress(self.finished, None)
-                n, more = int(buf[0]), int(buf[2])
+                if isinstance(buf, list):  # several rounds per call: leaves summed, the last round's `left`
+                    n, more = sum(int(b[0]) for b in buf), int(buf[-1][2])
+                else:
+                    n, more = int(buf[0]), int(buf[2])
                 rc.n = n
                 ln.leaves += n
                 if n > 0:
@@ -417,7 +428,11 @@ class SelfPlay:
         env = os.environ.get("UTTT_ROUND_LOOKAHEAD")
         if env:
             return max(1, int(env))
-        return 3 if all(getattr(ln.evaluator, "cheap", False) for ln in self.lanes) else 1
+        if not all(getattr(ln.evaluator, "cheap", False) for ln in self.lanes):
+            return 1
+        # calls in flight: their rounds' ring slots must not be reused before the call is read (8 slots)
+        r = max(getattr(ln.evaluator, "rounds_per_call", 1) for ln in self.lanes)
+        return 3 if r == 1 else max(1, 8 // r)
 
     def _enqueue_round(self, ln, spec):
         """Select of one round on the lane's stream, its counts stored by the scan into a slot of the
@@ -428,12 +443,17 @@ class SelfPlay:
         rc = RoundCount()
         slot = ln.ring_pos % len(ln.count_ring)
         buf = ln.count_ring[slot]
-        ln.ring_pos += 1
         one_call = getattr(ln.evaluator, "round_async", None)
         if spec and one_call is not None:
-            # the whole round in one C call, on the engine's stream; readiness is the tag the scan stores
-            # into the ring slot after the counts (no event, no torch stream context per round)
-            return rc, _TagReady(buf, one_call(ln.engine, slot)), spec, buf
+            # whole rounds in one C call, on the engine's stream; readiness is the tag the last round stores
+            # into its ring slot after the counts (no event, no torch stream context per round). With several
+            # rounds per call, the counts of the call's slots are summed (the last one's `left` decides)
+            r = getattr(ln.evaluator, "rounds_per_call", 1)
+            ln.ring_pos += r
+            slots = [ln.count_ring[(slot + i) % len(ln.count_ring)] for i in range(r)]
+            last = slots[-1]
+            return rc, _TagReady(last, one_call(ln.engine, slot)), spec, (slots if r > 1 else last)
+        ln.ring_pos += 1
         with self._ctx(ln):
             # readiness: the tag the scan stores into the ring slot after the counts (round 5; a torch event
             # per round before)
