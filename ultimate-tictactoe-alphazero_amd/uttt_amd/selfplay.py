@@ -46,10 +46,11 @@ class HashEvaluator:
         dev = torch.device("cuda", engine.device)
         self.policy = torch.zeros((engine.max_trees, 81), dtype=torch.float32, device=dev)
         self.value = torch.zeros((engine.max_trees, 1), dtype=torch.float32, device=dev)
-        # rounds per C call (round 6): each call enqueues this many one-dispatch rounds and the host polls only
-        # the last one's tag, so the host's per-round reaction (the tree-only bound) is paid once per call;
-        # rounds past the move's end find every tree done. UTTT_ROUND_BATCH (1 = one round per call).
-        self.rounds_per_call = max(1, min(4, int(os.environ.get("UTTT_ROUND_BATCH", "4"))))
+        # rounds per C call (UTTT_ROUND_BATCH, default 1): a call may enqueue up to 4 one-dispatch rounds whose
+        # last tag alone is polled, but the rounds enqueued past a move's end then outnumber the host time
+        # saved: tree-only 4096 x 50, interleaved (profiles/r6/sweeps/u6j): 1 round per call, 3 in flight
+        # 558-567M sims/s; 2 x 3 509-511M; 2 x 4 471-472M; 4 x 2 508-509M; 1 x 4 548-551M
+        self.rounds_per_call = max(1, min(4, int(os.environ.get("UTTT_ROUND_BATCH", "1"))))
 
     def round_async(self, engine, slot):
         """rounds_per_call whole rounds in one C call (Engine.rounds_hash_async: per round one k_round1 launch
