@@ -321,6 +321,7 @@ class SelfPlay:
                     progress(self.finished, None)
             return total
         depth = self._lookahead()
+        spin = depth > 1 and os.environ.get("UTTT_POLL_SLEEP", "0") != "1"
         for ln in self.lanes:
             if ln.count_ring is None:
                 ln.count_ring = ln.engine.count_ring()  # the scan writes each round's counts here
@@ -351,7 +352,10 @@ class SelfPlay:
             # turn would leave the other lane's stream empty once it runs ahead)
             ready = [key for key in state if state[key][1][0][1].query()]
             if not ready:
-                time.sleep(2e-5)
+                # cheap rounds (the hash evaluator, ~30 us each): spin, since a 20-us sleep lasts 60-100 us on
+                # Linux and the three rounds in flight drain meanwhile (UTTT_POLL_SLEEP=1 sleeps as before)
+                if not spin:
+                    time.sleep(2e-5)
                 continue
             for key in ready:
                 ln, q = state[key]
