@@ -170,6 +170,23 @@ def test_selfplay_matches_oracle_and_is_slot_invariant(gpu, oracle_lib):
             assert np.array_equal(r["values"], ref[g]["values"].astype(np.int64))
 
 
+@pytest.mark.parametrize("batch", ["2", "4"])
+def test_batched_hash_rounds_change_no_record(gpu, oracle_lib, batch, monkeypatch):
+    """Several one-dispatch hash rounds per host call (UTTT_ROUND_BATCH; the rounds enqueued past a move's
+    end find every tree done): records still equal the oracle's bit for bit, with two lanes too."""
+    monkeypatch.setenv("UTTT_ROUND_BATCH", batch)
+    n_games, seed = 12, 808
+    ref = [oracle_lib.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
+    for lanes in (1, 2):
+        sp = gpu.SelfPlay(8, 30, 4, 1.0, lanes=lanes)
+        sp.run(0, n_games, seed)
+        recs = sp.records()
+        assert len(recs) == n_games
+        for g, r in enumerate(recs):
+            assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (batch, lanes, g)
+            assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64))
+
+
 @pytest.mark.parametrize("budget", ["1", "3"])
 def test_select_budget_changes_no_record(gpu, oracle_lib, budget, monkeypatch):
     """UTTT_SELECT_BUDGET (in-place completions per tree and k_select launch) only spreads a move's
