@@ -191,6 +191,9 @@ int uttt_search1_next(uttt_engine_t *eng, uttt_state_t *leaf, int32_t *copies, i
 int uttt_search1_apply(uttt_engine_t *eng, const float *policy, int64_t policy_stride, const float *value,
                        int32_t rows);
 int uttt_search1_scores(uttt_engine_t *eng, float *scores, int32_t *n_legal);
+/* Diagnostics (no reference counterpart): the resident wave's own time split up to its last hand-over, in
+ * 10 ns ticks since its launch: [0] descents, [1] applies, [2] waits for the host's commands. */
+int uttt_search1_time_split(uttt_engine_t *eng, int32_t *ticks3);
 
 /* Evaluator results for the pending leaves (uttt_mcts.cpp:138-167: legal-mask,
  * sequential f32 renormalisation, expand k times, back up k times).

@@ -453,6 +453,43 @@ def test_uttt_cpp_resident_search_resumes_and_recovers(gpu):
     assert np.array_equal(sc.view(np.uint32), d["scores"][r][:n].view(np.uint32))
 
 
+def test_uttt_cpp_distinct_copy_results_match_oracle(gpu, oracle_lib):
+    """The reference applies each queued copy's own result in order (uttt_mcts.cpp:138-167). A model whose
+    result changes with every state it is handed (a hash salted by a running count) gives each copy of a
+    flush a different row; the resident search (k_search1, rows loaded in chunks of 8) must equal the oracle
+    bit for bit, at batches above and below the chunk (k up to 16: a second chunk is reloaded)."""
+    import uttt_cpp
+    from oracle import core
+    from oracle.hashnp import hash_eval_np
+    _, ostates = _random_positions(core, 6, 4242)
+    for S, B, T in ((50, 8, 1.0), (30, 3, 0.5), (100, 16, 1.0), (60, 12, 0.0)):
+        for os_ in ostates:
+            cnt = [0]
+
+            def oracle_eval(x):
+                cnt[0] += 1
+                return hash_eval_np(np.asarray(x, np.float32), 0x9E3779B9 + cnt[0])
+
+            ref_sc, _, st = core.pv_mcts_scores(os_, T, S, B, oracle_eval)
+            n_ref = cnt[0]
+            cnt[0] = 0
+
+            def model(states):
+                out = []
+                for s in states:
+                    x = np.asarray(s.to_input_tensor(), np.float32).reshape(9, 9, 3).transpose(2, 0, 1)
+                    out.append(oracle_eval(x.reshape(-1)))
+                return [(p, float(v)) for p, v in out]
+
+            p, e, mp, me, a = os_.arrays()
+            st_ = uttt_cpp.State(np.asarray(p).reshape(9, 9).tolist(), np.asarray(e).reshape(9, 9).tolist(),
+                                 [int(v) for v in mp], [int(v) for v in me], int(a))
+            sc = np.asarray(uttt_cpp.pv_mcts_scores(model=model, state=st_, temperature=T, evaluate_count=S,
+                                                    batch_size=B), np.float32)
+            assert cnt[0] == n_ref == st.evals
+            assert np.array_equal(sc.view(np.uint32), np.asarray(ref_sc, np.float32).view(np.uint32)), (S, B, T)
+
+
 def test_network_gpu_matches_cpu_fp32(gpu):
     """Value within 1e-5 of CPU fp32 (north star). The random-init net is saturated
     (|logits| up to ~1e2..1e3), so the policy is checked on its logits, relative to

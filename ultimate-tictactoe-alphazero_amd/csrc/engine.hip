@@ -1247,7 +1247,16 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
                                            int64_t pld, const float *__restrict__ value, int64_t vld,
                                            const int32_t *__restrict__ rowbase, int per_copy,
                                            unsigned long long *bytes_ctr, int slot, float *row /* LDS, 84 floats */,
-                                           int by_tree = -1, int by_tree_depth = 0) {
+                                           int by_tree = -1, int by_tree_depth = 0, float *copy_rows = nullptr,
+                                           bool host_rows = false) {
+    // copy_rows (LDS, 8 x 84 floats, 16-B aligned; optional): the per-copy prior sums of a chunk run in 8 lanes
+    // at once instead of one copy after another. host_rows: the evaluation rows sit in fine-grained host
+    // memory the host wrote behind a polled command; they are read with system-coherent (sc0 sc1) loads,
+    // so no cache invalidation stands between the command and them (k_search1: one leaf, its rows from row 0,
+    // at least 8 rows readable)
+    auto ld_row = [host_rows](const float *a) -> float {
+        return host_rows ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : *a;
+    };
     const int lane = lane_id();
     // two dependent round trips before the work: the count with this slot's tree and leaf depth
     // (tree_of / depth_of hold n_trees entries, stale past the count), then the tree's records, the
@@ -1263,6 +1272,19 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
         t = tr.tree_of[slot < tr.n_trees ? slot : 0];
         dq = tr.depth_of[slot < tr.n_trees ? slot : 0];
         if (slot >= cnt) return;
+    }
+    // host_rows, per copy: the first 8 rows (the host block holds at least 16) are loaded before the tree's
+    // records, whose round trip they then share; masked by legality and by k once those have arrived
+    constexpr int kCopyChunk = 8;
+    float h0[kCopyChunk], h1[kCopyChunk], hv[kCopyChunk];
+    if (host_rows && per_copy) {
+#pragma unroll
+        for (int jj = 0; jj < kCopyChunk; ++jj) {
+            const float *pol = policy + (int64_t)jj * pld;
+            h0[jj] = ld_row(pol + lane);
+            h1[jj] = ld_row(pol + 64 + (lane < 17 ? lane : 16));
+            hv[jj] = ld_row(value + (int64_t)jj * vld);
+        }
     }
     const LeafRec r = tr.rec[t];
     TreeCtl ctl = tr.ctl[t];
@@ -1283,9 +1305,9 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
     float raw0 = 0.0f, raw1 = 0.0f, rawv = 0.0f;
     if (!per_copy) {
         const float *pol = policy + (int64_t)slot * pld;
-        raw0 = pol[lane];
-        raw1 = pol[64 + (lane < 17 ? lane : 16)];
-        rawv = value[(int64_t)slot * vld];
+        raw0 = ld_row(pol + lane);
+        raw1 = ld_row(pol + 64 + (lane < 17 ? lane : 16));
+        rawv = ld_row(value + (int64_t)slot * vld);
     }
     const int depth = r.depth;
     const int k = r.k;
@@ -1345,12 +1367,68 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
             }
             return;
         }
+        // the copies' rows in chunks of kCopyChunk whose loads are all issued before the first use: one
+        // memory round trip per chunk instead of one per copy (the rows of a one-tree search sit in host
+        // memory, a PCIe round trip each: round 6 measured 16 us of a flush's apply on 8 sequential rows)
+        const int64_t rb = rowbase[slot];
+        float c0[kCopyChunk], c1[kCopyChunk], cv[kCopyChunk];
+        auto load_chunk = [&](int j0) {
+            if (host_rows && j0 == 0) {  // the prefetched rows (row base 0)
+#pragma unroll
+                for (int jj = 0; jj < kCopyChunk; ++jj) {
+                    const int q = jj < k ? jj : 0;
+                    float x0 = h0[0], x1 = h1[0], xv = hv[0];
+#pragma unroll
+                    for (int i = 1; i < kCopyChunk; ++i) {
+                        x0 = q == i ? h0[i] : x0;
+                        x1 = q == i ? h1[i] : x1;
+                        xv = q == i ? hv[i] : xv;
+                    }
+                    c0[jj] = l0 ? x0 : 0.0f;
+                    c1[jj] = l1 ? x1 : 0.0f;
+                    cv[jj] = xv;
+                }
+                return;
+            }
+#pragma unroll
+            for (int jj = 0; jj < kCopyChunk; ++jj) {
+                const int64_t row = rb + (j0 + jj < k ? j0 + jj : j0);
+                const float *pol = policy + row * pld;
+                c0[jj] = l0 ? ld_row(pol + lane) : 0.0f;
+                c1[jj] = l1 ? ld_row(pol + 64 + lane) : 0.0f;
+                cv[jj] = ld_row(value + row * vld);
+            }
+        };
+        // copy_rows: lane jj's sum of the chunk's copy jj, its legal priors compacted in action order into an
+        // LDS row (seq_sum_legal's order and zero padding, so the same f32 sum as the one-lane loop below)
+        const int L4 = (L + 3) & ~3;
+        float csum = 0.0f;
+        auto chunk_sums = [&]() {
+#pragma unroll
+            for (int jj = 0; jj < kCopyChunk; ++jj) {
+                float *rw = copy_rows + jj * 84;
+                if (l0) rw[i0] = c0[jj];
+                if (l1) rw[i1] = c1[jj];
+                if (lane >= L && lane < L4) rw[lane] = 0.0f;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's stores before any lane's reads
+            const float4 *r4 = reinterpret_cast<const float4 *>(copy_rows + (lane & (kCopyChunk - 1)) * 84);
+            float acc = 0.0f;
+            for (int i = 0; i < L4 / 4; ++i) {
+                const float4 q = r4[i];
+                acc += q.x;
+                acc += q.y;
+                acc += q.z;
+                acc += q.w;
+            }
+            csum = acc;
+        };
         bool bad = false;  // any copy's legal prior or value non-finite: nothing is applied (as above)
-        for (int j = 0; j < k; ++j) {
-            const int64_t row = (int64_t)rowbase[slot] + j;
-            const float *pol = policy + row * pld;
-            bad |= (l0 && !__builtin_isfinite(pol[lane])) || (l1 && !__builtin_isfinite(pol[64 + lane])) ||
-                   !__builtin_isfinite(value[row * vld]);
+        for (int j0 = 0; j0 < k; j0 += kCopyChunk) {
+            load_chunk(j0);
+#pragma unroll
+            for (int jj = 0; jj < kCopyChunk; ++jj)
+                bad |= !__builtin_isfinite(c0[jj]) || !__builtin_isfinite(c1[jj]) || !__builtin_isfinite(cv[jj]);
         }
         if (__ballot(bad)) {
             if (lane == 0) {
@@ -1362,20 +1440,29 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
         uint4 r_lo = pr_lo, r_hi = pr_hi;
         float w_lo = __uint_as_float(r_lo.x), w_hi = __uint_as_float(r_hi.x);
         for (int j = 0; j < k; ++j) {
-            const int64_t row = (int64_t)rowbase[slot] + j;
-            const float *pol = policy + row * pld;
-            const float p0 = l0 ? pol[lane] : 0.0f;
-            const float p1 = l1 ? pol[64 + lane] : 0.0f;
+            const int jj = j & (kCopyChunk - 1);
+            if (jj == 0 && k > kCopyChunk) load_chunk(j);  // k <= kCopyChunk: the check's chunk is still held
+            if (jj == 0 && copy_rows) chunk_sums();
+            float p0 = c0[0], p1 = c1[0], v = cv[0];
+#pragma unroll
+            for (int i = 1; i < kCopyChunk; ++i) {
+                p0 = jj == i ? c0[i] : p0;
+                p1 = jj == i ? c1[i] : p1;
+                v = jj == i ? cv[i] : v;
+            }
             float sum = 0.0f;
-            for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
-            for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+            if (copy_rows) {
+                sum = readlane_f(csum, jj);
+            } else {
+                for (uint64_t bits = b0; bits; bits &= bits - 1ull) sum += readlane_f(p0, __builtin_ctzll(bits));
+                for (uint64_t bits = b1; bits; bits &= bits - 1ull) sum += readlane_f(p1, __builtin_ctzll(bits));
+            }
             const float un = 1.0f / (float)L;
             const float q0 = sum > 0 ? p0 / sum : un;
             const float q1 = sum > 0 ? p1 / sum : un;
             const size_t blk = base + nb + (size_t)j * L;
             if (l0) pool.rec[blk + i0] = new_child(q0, (uint32_t)lane);
             if (l1) pool.rec[blk + i1] = new_child(q1, (uint32_t)(64 + lane));
-            const float v = value[row * vld];
             if (lane <= depth) w_lo += ((depth - lane) & 1) ? -v : v;
             if (lane + 64 <= depth) w_hi += ((depth - lane - 64) & 1) ? -v : v;
         }
@@ -1733,21 +1820,39 @@ struct Search1Host {
     // device -> host
     int32_t tag, count, k, status;  // a leaf (count 1) or the end (count 0); status: the tree's error bits
     int32_t n_legal, gone, pad0, pad1;  // gone: the command sequence the wave timed out waiting for (0: none)
+    // the wave's time split (s_memrealtime ticks of 10 ns, this launch): descents, applies, waits for the host
+    int32_t t_select, t_apply, t_wait, pad3;
     uttt_state_t leaf;
-    float scores[81];
-    // host -> device
-    int32_t cmd_seq, cmd_rows, cmd_exit, pad2;
-    // the evaluation rows: policy [rows][96] (81 used), value [rows], row base 0 (one leaf)
+    float scores[84];  // 81 used
+    // host -> device: the command, sequence (low word) and rows (high word) in one 8-byte store the wave
+    // reads whole; the exit word
+    uint64_t cmd;
+    int32_t cmd_exit, pad2;
+    // the evaluation rows: policy [rows][96] (81 used), value [rows] (one leaf: its row base is 0)
 };
+static_assert(offsetof(Search1Host, cmd) % 8 == 0, "Search1Host::cmd must be 8-byte aligned");
+
+// Stores to the host block: system-coherent (sc0 sc1) and relaxed. A hand-off is these stores, one
+// s_waitcnt vmcnt(0) (they are acknowledged), then the tag, also relaxed: no release fence, whose L2
+// write-back (buffer_wbl2) would flush the tree's dirty lines at every flush (the host reads only this block)
+__device__ __forceinline__ void st_host(int32_t *a, int32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_host(float *a, float v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void host_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 constexpr int kSearch1Timeout = 10000000;  // 100 ms of s_memrealtime (100 MHz)
 
 template <bool PY>
 __global__ __launch_bounds__(kWave) void k_search1(Pool pool, Trees tr, EvalCache cache, uttt_state_t root,
                                                    float temperature, Search1Host *hs, const float *policy,
-                                                   const float *value, const int32_t *rowbase, int32_t seq,
-                                                   int32_t resume) {
+                                                   const float *value, int32_t seq, int32_t resume) {
     __shared__ __attribute__((aligned(16))) float s_row[84];
+    __shared__ int32_t s_rowbase;  // the flush's first row: 0 (in LDS, not a PCIe round trip per apply)
+    __shared__ __attribute__((aligned(16))) float s_copies[8 * 84];  // per-copy rows' prior sums (apply_wave)
     const int lane = lane_id();
+    if (lane == 0) s_rowbase = 0;
     if (!resume) {  // k_begin's body for tree 0 (root expanded with uniform priors; py semantics: plain root)
         uint32_t m[3];
         legal_mask(root, m);
@@ -1785,19 +1890,29 @@ __global__ __launch_bounds__(kWave) void k_search1(Pool pool, Trees tr, EvalCach
         wave_memory_fence();
     }
     bool apply = resume != 0;  // resume: the command of sequence `seq` is waiting in host memory
+    int rows = resume ? (int)__builtin_amdgcn_readfirstlane((int)(
+                            __hip_atomic_load(&hs->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32))
+                      : 0;
+    uint64_t tk_sel = 0, tk_apply = 0, tk_wait = 0, tk = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (apply) {
-            const int rows = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&hs->cmd_rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
             // per-copy rows bypass the evaluation cache (as host_apply_args)
             EvalCache acache = cache;
             if (rows > 1) acache.flag = nullptr;
-            apply_wave(pool, tr, acache, policy, 96, value, 1, rowbase, rows > 1 ? 1 : 0, nullptr, 0, s_row, 0,
-                       __builtin_amdgcn_readfirstlane(tr.pending[0]) >> 8);
+            apply_wave(pool, tr, acache, policy, 96, value, 1, &s_rowbase, rows > 1 ? 1 : 0, nullptr, 0, s_row, 0,
+                       __builtin_amdgcn_readfirstlane(tr.pending[0]) >> 8, s_copies, true);
             wave_memory_fence();  // the descent reads the records the apply wrote
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            tk_apply += t1 - tk;
+            tk = t1;
         }
         const int p = select_wave<PY>(pool, tr, cache, nullptr, 0, s_row, nullptr, 0);
         const int q = p & 0xFF;
+        {
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            tk_sel += t1 - tk;
+            tk = t1;
+        }
         if (q == 2) {  // stopped by the select budget before a leaf: descend again (as uttt_search_select_host)
             apply = false;
             continue;
@@ -1805,39 +1920,48 @@ __global__ __launch_bounds__(kWave) void k_search1(Pool pool, Trees tr, EvalCach
         ++seq;
         if (q == 1 || q == 3) {  // a leaf: hand it to the host
             wave_memory_fence();
+            // the leaf (lanes 0-7, one store), its copies, the count and the time split, then the tag
+            const int32_t lw = reinterpret_cast<const int32_t *>(&tr.leaf[0])[lane & 7];
+            if (lane < 8) st_host(reinterpret_cast<int32_t *>(&hs->leaf) + lane, lw);
             if (lane == 0) {
-                const uttt_state_t lf = tr.leaf[0];
-                const int32_t *w = reinterpret_cast<const int32_t *>(&lf);
-                int32_t *d = reinterpret_cast<int32_t *>(&hs->leaf);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&hs->k, tr.rec[0].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&hs->count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&hs->tag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                st_host(&hs->k, tr.rec[0].k);
+                st_host(&hs->t_select, (int32_t)tk_sel);
+                st_host(&hs->t_apply, (int32_t)tk_apply);
+                st_host(&hs->t_wait, (int32_t)tk_wait);
+                st_host(&hs->count, 1);
             }
-            // wait for the host's command of this sequence (its rows were written before it)
+            host_stores_done();
+            if (lane == 0) st_host(&hs->tag, seq);
+            // wait for the host's command of this sequence (its rows were written before it; they are read
+            // with system-coherent loads, so the poll needs no acquire and its cache invalidation)
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             int got = 0;
             for (;;) {
-                int c = 0, x = 0;
+                uint64_t c = 0;
+                int x = 0;
                 if (lane == 0) {
-                    c = __hip_atomic_load(&hs->cmd_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    c = __hip_atomic_load(&hs->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     x = __hip_atomic_load(&hs->cmd_exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
-                c = __builtin_amdgcn_readfirstlane(c);
+                const int cs = __builtin_amdgcn_readfirstlane((int)(uint32_t)c);
                 x = __builtin_amdgcn_readfirstlane(x);
-                if (c == seq) {
+                if (cs == seq) {
+                    rows = __builtin_amdgcn_readfirstlane((int)(c >> 32));
                     got = 1;
                     break;
                 }
                 if (x) break;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)kSearch1Timeout) {
-                    if (lane == 0) __hip_atomic_store(&hs->gone, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (lane == 0) st_host(&hs->gone, seq);
+                    host_stores_done();
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
             if (!got) return;
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            tk_wait += t1 - tk;
+            tk = t1;
             apply = true;
             continue;
         }
@@ -1848,15 +1972,17 @@ __global__ __launch_bounds__(kWave) void k_search1(Pool pool, Trees tr, EvalCach
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         L = __builtin_amdgcn_readfirstlane(L);
-        for (int i = lane; i < 81; i += kWave)
-            __hip_atomic_store(&hs->scores[i], i < L ? s_row[i] : 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int i = lane; i < 81; i += kWave) st_host(&hs->scores[i], i < L ? s_row[i] : 0.0f);
         if (lane == 0) {
-            __hip_atomic_store(&hs->n_legal, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&hs->status, (int32_t)(tr.ctl[0].status & kErrMask), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&hs->count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&hs->tag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            st_host(&hs->n_legal, L);
+            st_host(&hs->t_select, (int32_t)tk_sel);
+            st_host(&hs->t_apply, (int32_t)tk_apply);
+            st_host(&hs->t_wait, (int32_t)tk_wait);
+            st_host(&hs->status, (int32_t)(tr.ctl[0].status & kErrMask));
+            st_host(&hs->count, 0);
         }
+        host_stores_done();
+        if (lane == 0) st_host(&hs->tag, seq);
         return;
     }
 }
@@ -2344,7 +2470,7 @@ struct uttt_engine {
     bool dev_apply_staged = false;
     bool dev_apply_by_tree = false;  // staged by a one-dispatch round (k_round1): rows by tree, no scan
     // the resident one-tree search (uttt_search1_*, k_search1): its host block and evaluation rows
-    Search1Host *h_s1 = nullptr;  // fine-grained pinned: Search1Host, then policy [cap][96], value [cap], row base
+    Search1Host *h_s1 = nullptr;  // fine-grained pinned: Search1Host, then policy [cap][96], value [cap]
     int32_t s1_cap = 0, s1_seq = 0;
     bool s1_alive = false;  // a k_search1 wave may still be resident on the stream
     uttt_state_t s1_root{};
@@ -2910,7 +3036,6 @@ static int flush_host_apply(uttt_engine *e) {
 // ---- the resident one-tree search (k_search1) ----
 static float *s1_policy(uttt_engine *e) { return reinterpret_cast<float *>(e->h_s1 + 1); }
 static float *s1_value(uttt_engine *e) { return s1_policy(e) + (size_t)e->s1_cap * 96; }
-static int32_t *s1_rowbase(uttt_engine *e) { return reinterpret_cast<int32_t *>(s1_value(e) + e->s1_cap); }
 
 // a resident wave left by an unfinished search exits (its exit word) before anything else runs on the stream
 static int search1_stop(uttt_engine *e) {
@@ -2924,7 +3049,7 @@ static int search1_stop(uttt_engine *e) {
 static int search1_launch(uttt_engine *e, int32_t resume) {
     hipLaunchKernelGGL(e->tr.py ? k_search1<true> : k_search1<false>, dim3(1), dim3(kWave), 0, e->stream, e->pool, e->tr,
                        e->cache, e->s1_root, e->s1_temperature, e->h_s1, (const float *)s1_policy(e),
-                       (const float *)s1_value(e), (const int32_t *)s1_rowbase(e), e->s1_seq, resume);
+                       (const float *)s1_value(e), e->s1_seq, resume);
     e->s1_alive = true;
     return check_launch();
 }
@@ -2957,10 +3082,9 @@ int uttt_search1_begin(uttt_engine_t *e, const uttt_state_t *root, int32_t sims,
     Search1Host *h = e->h_s1;
     h->tag = 0;
     h->gone = 0;
-    h->cmd_seq = 0;
+    h->cmd = 0;
     h->cmd_exit = 0;
     h->count = 0;
-    s1_rowbase(e)[0] = 0;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     e->s1_root = *root;
     e->s1_temperature = temperature;
@@ -3046,9 +3170,9 @@ int uttt_search1_apply(uttt_engine_t *e, const float *policy, int64_t pld, const
         memcpy(hp + (size_t)r * 96, policy + (size_t)r * pld, 81 * sizeof(float));
         hv[r] = value[r];
     }
-    __atomic_store_n(&h->cmd_rows, rows, __ATOMIC_RELAXED);
-    __atomic_thread_fence(__ATOMIC_SEQ_CST);  // the rows before the command the wave polls
-    __atomic_store_n(&h->cmd_seq, e->s1_seq, __ATOMIC_RELEASE);
+    // the rows before the command the wave polls (x86 keeps stores in order; the fence keeps the compiler's)
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    __atomic_store_n(&h->cmd, (uint64_t)(uint32_t)rows << 32 | (uint32_t)e->s1_seq, __ATOMIC_RELEASE);
     e->phase = 1;
     e->n_pending = 0;
     return UTTT_OK;
@@ -3064,6 +3188,15 @@ int uttt_search1_scores(uttt_engine_t *e, float *scores, int32_t *n_legal) {
     const int L = h->n_legal;
     for (int i = 0; i < 81; ++i) scores[i] = i < L ? h->scores[i] : 0.0f;
     *n_legal = L;
+    return UTTT_OK;
+}
+
+int uttt_search1_time_split(uttt_engine_t *e, int32_t *ticks3) {
+    if (!e || !ticks3 || !e->h_s1) return UTTT_ERR_ARG;
+    const Search1Host *h = e->h_s1;
+    ticks3[0] = __atomic_load_n(&h->t_select, __ATOMIC_ACQUIRE);
+    ticks3[1] = __atomic_load_n(&h->t_apply, __ATOMIC_ACQUIRE);
+    ticks3[2] = __atomic_load_n(&h->t_wait, __ATOMIC_ACQUIRE);
     return UTTT_OK;
 }
 

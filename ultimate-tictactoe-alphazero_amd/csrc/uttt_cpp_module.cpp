@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include <array>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -98,15 +99,16 @@ SearchEngine &search_engine() {
 void read_result(const py::handle &item, float *policy81, float *value) {
     py::tuple tup = py::reinterpret_borrow<py::object>(item).cast<py::tuple>();
     py::object pol = tup[0];
-    std::vector<float> p;
     if (py::isinstance<py::array>(pol)) {
         auto arr = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(pol);
         if (!arr) throw py::type_error("policy must be convertible to float32");
-        p.assign(arr.data(), arr.data() + arr.size());
+        const int n = (int)std::min<py::ssize_t>(arr.size(), 81);
+        std::memcpy(policy81, arr.data(), (size_t)n * sizeof(float));
+        for (int a = n; a < 81; ++a) policy81[a] = 0.0f;  // uttt_mcts.cpp:149
     } else {
-        p = pol.cast<std::vector<float>>();
+        const std::vector<float> p = pol.cast<std::vector<float>>();
+        for (int a = 0; a < 81; ++a) policy81[a] = a < (int)p.size() ? p[a] : 0.0f;
     }
-    for (int a = 0; a < 81; ++a) policy81[a] = a < (int)p.size() ? p[a] : 0.0f;  // uttt_mcts.cpp:149
     *value = tup[1].cast<float>();
 }
 
@@ -286,4 +288,13 @@ PYBIND11_MODULE(_uttt_cpp, m) {
             return out;
         },
         py::arg("xs"), py::arg("temperature"), "Apply Boltzmann distribution");
+    m.def(
+        "_search1_time_split",
+        [] {
+            int32_t t[3] = {0, 0, 0};
+            uttt_engine_t *eng = search_engine().eng;
+            if (eng) check(uttt_search1_time_split(eng, t));
+            return std::vector<double>{t[0] * 1e-5, t[1] * 1e-5, t[2] * 1e-5};
+        },
+        "Diagnostics: the last resident search's device time in ms (descents, applies, waits for the host)");
 }
