@@ -18,7 +18,7 @@ def main():
     from uttt_amd import SelfPlay
     from uttt_amd.model import FoldedDualNetwork, random_network
     games = int(os.environ.get("GAMES", 4096))
-    age = int(os.environ.get("AGE", 120))
+    age = int(os.environ.get("AGE", 60))
     steps = int(os.environ.get("STEPS", 20))
     net = FoldedDualNetwork(random_network(0, "cuda")).cuda()
     stats = {"calls": 0, "rows": 0, "unique": 0}
@@ -41,7 +41,9 @@ def main():
     sp = SelfPlay(games, 50, 8, 1.0, device=0, cache_log2=23, lanes=1)
     sp.set_evaluator(make)
     sp.begin(0, (age + steps + 2) * games, 1234, arena_plies=(age + steps + 2) * games)
-    sp.steps(age)
+    for i in range(0, age, 10):
+        sp.steps(min(10, age - i))
+        print(f"aged {i + 10}", flush=True)
     counting[0] = True
     sp.steps(steps)
     torch.cuda.synchronize()

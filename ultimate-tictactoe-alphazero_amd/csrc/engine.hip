@@ -271,6 +271,18 @@ __device__ __forceinline__ int wave_argmax(float v, int i, int cnt) {
 // read what one lane wrote; same CU, so workgroup scope suffices).
 __device__ __forceinline__ void wave_memory_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
+// Stores to host-visible (fine-grained pinned) words: system-coherent (sc0 sc1) and relaxed. A hand-off to
+// the host is these stores, one s_waitcnt vmcnt(0) (they are acknowledged), then the tag, also relaxed: no
+// release fence, whose L2 write-back (buffer_wbl2 sc0 sc1) would flush every line the kernel dirtied in the
+// XCD's L2 (tree records, rows) to HBM at each hand-off, when the host reads only these words (round 6)
+__device__ __forceinline__ void st_host(int32_t *a, int32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_host(float *a, float v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void host_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ------------------------------------------------------ evaluation cache --
 // Open-addressing table in HBM: position (32 B) -> raw evaluator output (81
 // priors + value, before legal masking). The evaluator is a pure function of
@@ -1098,7 +1110,8 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                 for (int i = 0; i < 8; ++i) __hip_atomic_store(d + i, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&host_leaf->k, tr.rec[t].k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            __hip_atomic_store(&host_leaf->tag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            host_stores_done();
+            st_host(&host_leaf->tag, tag);
         }
     }
     return __builtin_amdgcn_readfirstlane(pend);
@@ -1212,7 +1225,8 @@ __global__ __launch_bounds__(1024) void k_scan(Trees tr, unsigned long long *sta
             __hip_atomic_store(host_count + 0, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 1, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 2, c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_count + 3, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            host_stores_done();
+            st_host(host_count + 3, tag);
         }
     }
 }
@@ -1672,7 +1686,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
             __hip_atomic_store(host_count + 0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_count + 2, n2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_count + 3, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            host_stores_done();
+            st_host(host_count + 3, tag);
         }
     }
 }
@@ -1832,16 +1847,6 @@ struct Search1Host {
 };
 static_assert(offsetof(Search1Host, cmd) % 8 == 0, "Search1Host::cmd must be 8-byte aligned");
 
-// Stores to the host block: system-coherent (sc0 sc1) and relaxed. A hand-off is these stores, one
-// s_waitcnt vmcnt(0) (they are acknowledged), then the tag, also relaxed: no release fence, whose L2
-// write-back (buffer_wbl2) would flush the tree's dirty lines at every flush (the host reads only this block)
-__device__ __forceinline__ void st_host(int32_t *a, int32_t v) {
-    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_host(float *a, float v) {
-    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void host_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 constexpr int kSearch1Timeout = 10000000;  // 100 ms of s_memrealtime (100 MHz)
 
 template <bool PY>
