@@ -64,7 +64,7 @@ def main():
         return res
 
     mods = [("this_uttt_cpp_reference_glue", uttt_cpp, {"dedup": False}),
-            ("this_uttt_cpp_reference_glue_dedup", uttt_cpp, {})]
+            ("this_uttt_cpp_reference_glue_dedup", uttt_cpp, {"dedup": True})]
     if os.path.isdir(ref_dir):
         import importlib.machinery
         import importlib.util
