@@ -374,12 +374,29 @@ __device__ __forceinline__ rsrc_t rec_rsrc(const EvalCache &c, uint32_t slot) {
 // record read in one round trip (lanes 0-1 the key, checked against s; 2-22 the values), then the
 // flag is re-checked. On a hit the 82 values are copied to dst (LDS, 16-byte aligned, >= 84 floats)
 // and true is returned; a tag that matched another position's entry (a 16-bit collision) is a miss.
-__device__ bool cache_lookup(const EvalCache &c, const uttt_state_t &s, float *dst) {
+// The probe in two halves: the flags' loads are issued first, so work that does not need them (the select's
+// leaf checks) runs under their round trip (round 6)
+struct CacheProbe {
+    uint64_t h64;
+    uint32_t f;  // lane l < kProbe: flag of slot h + l
+};
+__device__ __forceinline__ CacheProbe cache_probe_issue(const EvalCache &c, const uttt_state_t &s) {
+    CacheProbe p;
+    p.h64 = 0ull;
+    p.f = 0u;
+    if (!c.flag) return p;
+    const int lane = (int)(threadIdx.x & 63);
+    p.h64 = state_hash64(s);
+    p.f = lane < kProbe ? ld_agent(c.flag + (((uint32_t)p.h64 + (uint32_t)lane) & c.mask)) : 0u;
+    return p;
+}
+
+__device__ bool cache_lookup_probed(const EvalCache &c, const CacheProbe &pr, const uttt_state_t &s, float *dst) {
     if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
-    const uint64_t h64 = state_hash64(s);
+    const uint64_t h64 = pr.h64;
     const uint32_t h = (uint32_t)h64, tag = state_tag(h64);
-    const uint32_t f = lane < kProbe ? ld_agent(c.flag + ((h + (uint32_t)lane) & c.mask)) : 0u;
+    const uint32_t f = pr.f;
     const uint64_t cand = __ballot(lane < kProbe && flag_ready(f) && flag_tag(f) == tag);
     const uint64_t empty = __ballot(lane < kProbe && f == 0u);
     if (!cand) return false;
@@ -984,6 +1001,9 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
             if (pa >= 0) s = next_state(s, pa);  // the leaf's state
             if (fail) break;
             levels += (unsigned int)(depth + 1);
+            // the evaluation cache's flags for this leaf are loaded before its terminal checks, which run
+            // under that round trip (a terminal leaf's probe is discarded)
+            const CacheProbe probe = cache_probe_issue(cache, s);
             const bool lose = is_lose(s);
             const bool no_legal = legal_count(s) == 0u;
             clk.mark<kSpLeaf>();
@@ -1022,7 +1042,7 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
             const int k = min(tr.batch, tr.sims - sims_done);
             float *cv = cv_row;
             trips += cache.flag ? 1 : 0;
-            const bool hit = cache_lookup(cache, s, cv);
+            const bool hit = cache_lookup_probed(cache, probe, s, cv);
             clk.mark<kSpProbe>();
             if (hit) {  // the flush's evaluation is already known: apply it now
                 trips += 4;
@@ -2030,6 +2050,7 @@ struct SelfPlay {
     GameEntry *games;
     int64_t *ctr;          // [0] next game id, [1] games finished, [2] arena plies used
     int32_t *live;         // [slot] flags for k_begin
+    int32_t *work;         // [1 + slot]: k_finalize's count, then the slots k_archive has work for
     int64_t game_end;
     int64_t arena_cap;
     int64_t games_cap;
@@ -2133,11 +2154,18 @@ __device__ __forceinline__ double row_entry(double x0, double x1, int i) {
 __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, const unsigned long long *err) {
     // asynchronous form: k_tree_err has folded the failed trees into *err; on a failure this move's
     // end changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
-    if (err && *err != ~0ull) return;
     const int lane = lane_id();
     const int s = wave_index();
     if (s >= sp.slots) return;
+    // the loads that do not depend on each other are issued together (round 6: the failure word, the slot,
+    // the key position and the root's record were four dependent round trips before the first draw)
+    const size_t base = (size_t)s * pool.cap;
+    const unsigned long long ev = err ? *err : ~0ull;
     Slot sl = sp.slot[s];
+    int32_t pos = sp.mt_pos[s];
+    int first;
+    const int L = root_children(pool, base, first);
+    if (ev != ~0ull) return;
     sl.finished = 0;
     if (!sl.live) {
         if (lane == 0) sp.slot[s] = sl;
@@ -2146,7 +2174,9 @@ __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, con
     // np.random.choice's random_sample (numpy legacy: two 32-bit draws, 53-bit double); a key that
     // runs out is twisted by the wave (mt_twist_wave)
     uint32_t *key = sp.mt_key + (size_t)s * 624;
-    int32_t pos = sp.mt_pos[s];
+    const bool h0 = lane < L, h1 = lane + 64 < L;
+    const int n0 = h0 ? visits_of(pool, base + first + lane) : 0;
+    const int n1 = h1 ? visits_of(pool, base + first + lane + 64) : 0;
     uint32_t w1, w2;
     if (pos >= 623) {
         const uint32_t k623 = key[623];
@@ -2166,14 +2196,8 @@ __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, con
         pos += 2;
     }
     const double u = ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
-    const size_t base = (size_t)s * pool.cap;
     const int ply = sl.ply;
-    // root visit counts (uttt_mcts.cpp:177-192, as root_scores): entry i in lane i / i - 64
-    int first;
-    const int L = root_children(pool, base, first);
-    const bool h0 = lane < L, h1 = lane + 64 < L;
-    const int n0 = h0 ? visits_of(pool, base + first + lane) : 0;
-    const int n1 = h1 ? visits_of(pool, base + first + lane + 64) : 0;
+    // root visit counts (uttt_mcts.cpp:177-192, as root_scores): entry i in lane i / i - 64 (loaded above)
     double x0, x1;
     if (sp.temperature == 0.0f) {
         // one-hot first max: the largest count, then the lowest index holding it (counts < 2^24, so
@@ -2286,11 +2310,15 @@ __device__ __forceinline__ void store_host_i64(int64_t *p, int64_t v) {
 }
 __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned long long *err, int64_t *host_move) {
     __shared__ unsigned long long wsum[16];
+    __shared__ int s_work;  // entries of k_archive's work list
     if (err && *err != ~0ull) {  // a failed tree: the move is not ended (k_move_end)
         if (host_move && threadIdx.x == 0) store_host_i64(host_move + 4, (int64_t)*err);
         return;
     }
     const int tid = threadIdx.x;
+    // the counters are read before the scans (only this kernel writes them, after its last barrier): their
+    // round trip overlaps the slots' instead of following the scans
+    const int64_t arena0 = sp.ctr[2], games0 = sp.ctr[1], next0 = sp.ctr[0];
     const int per = (sp.slots + 1023) / 1024;
     const int b = tid * per, e = min(b + per, sp.slots);
     // the scans need a slot's live / finished / fin_len only: one 16-byte load of Slot bytes 40..55 per slot
@@ -2321,12 +2349,13 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
     __syncthreads();  // wsum is reused
     const unsigned long long cnt_ex =
         block_scan_1024((unsigned long long)fr | ((unsigned long long)fc << 32), &cnt_tot, wsum);
-    const int64_t arena0 = sp.ctr[2], games0 = sp.ctr[1], next0 = sp.ctr[0];
     long long off = arena0 + (long long)fl_ex;
     int gi = (int)(games0 + (long long)(cnt_ex >> 32));
     int fi = (int)(cnt_ex & 0xFFFFFFFFull);
     const long long fin_total = (long long)fl_tot;
     const int free_total = (int)(cnt_tot & 0xFFFFFFFFull), fin_count = (int)(cnt_tot >> 32);
+    if (tid == 0) s_work = 0;
+    __syncthreads();
     for (int i = b; i < e; ++i) {
         const int4 h = hot_of(i);
         if (!h.z && h.y) continue;  // playing on: nothing here changes it
@@ -2366,9 +2395,13 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned l
         }
         sp.live[i] = sl.live;
         sp.slot[i] = sl;
+        // k_archive's work: a finished game to copy to the arena, or a new game's key to seed (about 1 in
+        // 40 slots per move, so k_archive runs a short list instead of a workgroup per slot)
+        if ((sl.finished && sl.fin_offset >= 0) || sl.seed_pending) sp.work[1 + atomicAdd(&s_work, 1)] = i;
     }
     __syncthreads();  // every thread read sp.ctr before it is rewritten
     if (tid == 0) {
+        sp.work[0] = s_work;
         sp.ctr[2] = arena0 + fin_total;
         sp.ctr[1] = games0 + fin_count;
         const int64_t nxt = next0 + free_total;
@@ -2402,38 +2435,45 @@ __device__ __forceinline__ void mt_seed_wave(uint32_t *key, int32_t *pos, uint32
     if (lane == 0) *pos = 624;
 }
 
-// Each block: one slot. The last wave seeds a refilled slot's key while the others copy a finished game's
-// plies, eight independent loads in flight per thread before their stores (the copy was one dependent
-// load-store pair per iteration: ~19 memory round trips per game, round 4's 39 us launch).
+// Each block: the slots of k_finalize's work list (entry w, w + grid, ...; round 6: a workgroup per slot
+// for the ~1 in 40 slots with work cost 24 us a move in dispatch alone). The last wave seeds a refilled
+// slot's key while the others copy a finished game's plies, eight independent loads in flight per thread
+// before their stores (the copy was one dependent load-store pair per iteration: ~19 memory round trips
+// per game, round 4's 39 us launch).
+constexpr int kArchiveBlocks = 256;
 __global__ __launch_bounds__(256) void k_archive(SelfPlay sp, const unsigned long long *err) {
     if (err && *err != ~0ull) return;
-    const int s = blockIdx.x;
-    const Slot sl = sp.slot[s];
-    const int wave = (int)threadIdx.x >> 6;
-    if (sl.seed_pending && wave == 3) {
-        mt_seed_wave(sp.mt_key + (size_t)s * 624, sp.mt_pos + s, sp.seed_base + (uint32_t)sl.game);
-        if (lane_id() == 0) sp.slot[s].seed_pending = 0;
-    }
-    if (!sl.finished || sl.fin_offset < 0) return;
-    const size_t src0 = (size_t)s * kMaxPlies, dst0 = (size_t)sl.fin_offset;
-    const double *__restrict__ from = sp.ply_policy + src0 * 81;
-    double *__restrict__ to = sp.ar_policy + dst0 * 81;
-    const int n = sl.fin_len * 81;  // the game's policy rows are contiguous in both places
-    constexpr int kU = 8;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 256 * kU) {
-        double v[kU];
+    const int n_work = sp.work[0];
+    for (int w = blockIdx.x; w < n_work; w += gridDim.x) {
+        const int s = sp.work[1 + w];
+        const Slot sl = sp.slot[s];
+        const int wave = (int)threadIdx.x >> 6;
+        if (sl.seed_pending && wave == 3) {
+            mt_seed_wave(sp.mt_key + (size_t)s * 624, sp.mt_pos + s, sp.seed_base + (uint32_t)sl.game);
+            if (lane_id() == 0) sp.slot[s].seed_pending = 0;
+        }
+        if (!sl.finished || sl.fin_offset < 0) continue;
+        const size_t src0 = (size_t)s * kMaxPlies, dst0 = (size_t)sl.fin_offset;
+        const double *__restrict__ from = sp.ply_policy + src0 * 81;
+        double *__restrict__ to = sp.ar_policy + dst0 * 81;
+        const int n = sl.fin_len * 81;  // the game's policy rows are contiguous in both places
+        constexpr int kU = 8;
+        for (int i0 = threadIdx.x; i0 < n; i0 += 256 * kU) {
+            double v[kU];
 #pragma unroll
-        for (int j = 0; j < kU; ++j) v[j] = i0 + 256 * j < n ? from[i0 + 256 * j] : 0.0;
+            for (int j = 0; j < kU; ++j) v[j] = i0 + 256 * j < n ? from[i0 + 256 * j] : 0.0;
 #pragma unroll
-        for (int j = 0; j < kU; ++j)
-            if (i0 + 256 * j < n) to[i0 + 256 * j] = v[j];
-    }
-    for (int ply = threadIdx.x; ply < sl.fin_len; ply += 256) {
-        sp.ar_state[dst0 + ply] = sp.ply_state[src0 + ply];
-        sp.ar_action[dst0 + ply] = sp.ply_action[src0 + ply];
-        sp.ar_value[dst0 + ply] = (int8_t)((ply & 1) ? -sl.fin_value : sl.fin_value);
+            for (int j = 0; j < kU; ++j)
+                if (i0 + 256 * j < n) to[i0 + 256 * j] = v[j];
+        }
+        for (int ply = threadIdx.x; ply < sl.fin_len; ply += 256) {
+            sp.ar_state[dst0 + ply] = sp.ply_state[src0 + ply];
+            sp.ar_action[dst0 + ply] = sp.ply_action[src0 + ply];
+            sp.ar_value[dst0 + ply] = (int8_t)((ply & 1) ? -sl.fin_value : sl.fin_value);
+        }
     }
 }
+static int archive_grid(int slots) { return slots < kArchiveBlocks ? slots : kArchiveBlocks; }
 
 __global__ void k_hwc(const uttt_state_t *st, int64_t n, float *out) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3537,7 +3577,7 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
             (rc = alloc_n(e, &sp.mt_pos, slots)) || (rc = alloc_n(e, &sp.ply_state, (size_t)slots * kMaxPlies)) ||
             (rc = alloc_n(e, &sp.ply_policy, (size_t)slots * kMaxPlies * 81)) ||
             (rc = alloc_n(e, &sp.ply_action, (size_t)slots * kMaxPlies)) || (rc = alloc_n(e, &sp.ctr, 4)) ||
-            (rc = alloc_n(e, &sp.live, slots)))
+            (rc = alloc_n(e, &sp.live, slots)) || (rc = alloc_n(e, &sp.work, (size_t)slots + 1)))
             return rc;
     }
     // every archived game has >= 1 ply, so the arena bounds the game table too
@@ -3570,7 +3610,7 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const unsigned long long *)nullptr,
                        (int64_t *)nullptr);
-    hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, sp, (const unsigned long long *)nullptr);
+    hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, sp, (const unsigned long long *)nullptr);
     if ((rc = check_launch())) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_move, sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -3632,7 +3672,7 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
         const unsigned long long *no_err = nullptr;
         hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, no_err);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, no_err, (int64_t *)nullptr);
-        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, no_err);
+        hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, e->sp, no_err);
     }
     if ((rc = check_launch())) return rc;
     int64_t ctr[4];
@@ -3698,7 +3738,7 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
         const unsigned long long *err = e->d_err;
         hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, err);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, err, e->h_move);
-        hipLaunchKernelGGL(k_archive, dim3(slots), dim3(256), 0, e->stream, e->sp, err);
+        hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, e->sp, err);
     }
     int rc = check_launch();
     if (rc) return rc;  // k_finalize stored the counters and the failure word into h_move
