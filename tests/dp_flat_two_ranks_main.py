@@ -84,7 +84,10 @@ if __name__ == "__main__":
                 gref = torch.cat([q.grad.reshape(-1) for q in ref.parameters() if q.requires_grad])
                 scale = max(gref.abs().max().item(), 1e-12)
                 err = (step.flat - gref).abs().max().item()
-                assert err <= 1e-3 * scale, (err, scale)
+                # train-mode BatchNorm over 16-sample rank batches amplifies the GPU's reduction-order rounding
+                # (max error / max gradient measured 0.8e-3 .. 1.6e-3 across boxes); a replay or all-reduce
+                # fault (a stale flat buffer, one rank's half missing) is an O(1) relative error
+                assert err <= 1e-2 * scale, (err, scale)
                 hist.append((round(lg, 6), round(le, 6), round(err / scale, 7)))
                 continue
             opt_r.step()

@@ -664,7 +664,10 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const cha
                                                   unsigned long long *err) {
     const int lane = lane_id();
     const int t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    if (err && t == 0 && lane == 0) *err = ~0ull;
+    if (t == 0 && lane == 0) {
+        if (err) *err = ~0ull;
+        tr.count[2] = -1;  // a search starts: no round of it is known to be empty yet (k_round1's fast exit)
+    }
     if (t >= tr.n_trees) return;
     const bool on = live ? (live[t] != 0) : true;
     const uttt_state_t s = *reinterpret_cast<const uttt_state_t *>(src + (size_t)t * src_stride);
@@ -1606,6 +1609,20 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
     __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];
     __shared__ uint32_t s_cnt;
     __shared__ int s_last;
+    // a round behind one that queued no leaf and left no tree with simulations (the host's look-ahead rounds
+    // past a move's end) has nothing to apply or select: every pending word is already 0 and the counts
+    // stay 0, so block 0 publishes them and its tag, and every other block leaves at once (round 6: such a
+    // round cost ~19 us of GPU time as a full pass over the trees; k_begin marks a new search non-empty)
+    if (tr.count[0] == 0 && tr.count[2] == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && host_count) {
+            st_host(host_count + 0, 0);
+            st_host(host_count + 1, 0);
+            st_host(host_count + 2, 0);
+            host_stores_done();
+            st_host(host_count + 3, tag);
+        }
+        return;
+    }
     const int t = wave_index();
     const int lane = lane_id();
     if (threadIdx.x == 0) s_cnt = 0u;
