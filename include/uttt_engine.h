@@ -217,7 +217,7 @@ int uttt_eval_hash_dev(uttt_engine_t *eng, float *policy, float *value);
  * one launch (k_round: per tree, the previous evaluation applied, then the next descent), and any
  * other call that reads the trees (the move's end, the root results, a synchronous select) applies
  * it first. UTTT_FUSED_ROUNDS=0 launches the three steps as written above. The scan stores the
- * round's counts and then `tag` (word 3 of the slot, a system-scope release store), so the host
+ * round's counts and then `tag` (word 3 of the slot; the counts' stores drained before it), so the host
  * learns that the counts landed by polling the tag: no event and no host sync per round. policy:
  * (max_trees, 81) f32, value: (max_trees,) f32, device memory, left untouched until the staged apply
  * has run. Replaces, for the test evaluator, one pass of the flush loop of uttt_mcts.cpp:109-167
@@ -228,6 +228,15 @@ int uttt_round_hash_async(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, fl
  * a round past the move's last finds every tree done and changes nothing. */
 int uttt_rounds_hash_async(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, float *policy, float *value,
                            int32_t n_rounds);
+/* A move's whole round loop in one call (round 6; replaces, for the test evaluator, the flush loop of
+ * uttt_mcts.cpp:109-167 run to the move's end over every tree, as self_play_cpp.play's per-move
+ * pv_mcts_scores call does): `depth` hash rounds kept in flight (uttt_round_hash_async, ring slots from
+ * ring_slot on, tags tag, tag + 1, ... masked to 31 bits), the host spinning on each round's tag in turn and
+ * enqueueing the next until a round reports no tree with simulations left. Returns when that round's
+ * counts landed; the rounds still in flight behind it are empty. *n_rounds: rounds enqueued (ring slots and
+ * tags consumed), *n_leaves: leaves evaluated, *n_with_leaves: rounds that had leaves. */
+int uttt_rounds_hash_move(uttt_engine_t *eng, int32_t ring_slot, int32_t tag, float *policy, float *value,
+                          int32_t depth, int32_t *n_rounds, int64_t *n_leaves, int32_t *n_with_leaves);
 
 /* Root results after the search: visit counts of the root's children (legal
  * order, row stride 81) and |legal| per tree. */

@@ -187,6 +187,29 @@ def test_batched_hash_rounds_change_no_record(gpu, oracle_lib, batch, monkeypatc
             assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64))
 
 
+def test_move_loop_in_c_equals_the_python_round_loop(gpu, oracle_lib, monkeypatch):
+    """One lane with the hash evaluator runs each move's round loop in one C call (uttt_rounds_hash_move,
+    SelfPlay._steps_move_loop); UTTT_MOVE_LOOP=0 keeps the Python round loop. Both give the oracle's records,
+    the same totals (simulations, rounds with leaves, leaves, finished games) and play the same moves per
+    steps(k) call."""
+    n_games, seed = 20, 909
+    ref = [oracle_lib.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
+    stats = {}
+    for loop in ("1", "0"):
+        monkeypatch.setenv("UTTT_MOVE_LOOP", loop)
+        sp = gpu.SelfPlay(6, 30, 4, 1.0)
+        sp.begin(0, n_games, seed)
+        per_call = [sp.steps(5) for _ in range(3)]
+        per_call.append(sp.steps())
+        recs = sp.records()
+        assert len(recs) == n_games
+        for g, r in enumerate(recs):
+            assert np.array_equal(r["actions"], ref[g]["actions"].astype(np.int64)), (loop, g)
+            assert np.array_equal(r["policies"].view(np.uint64), ref[g]["policies"].view(np.uint64)), (loop, g)
+        stats[loop] = (per_call, sp.sims, sp.rounds, sp.leaves, sp.finished, sp.moves)
+    assert stats["1"] == stats["0"]
+
+
 @pytest.mark.parametrize("budget", ["1", "3"])
 def test_select_budget_changes_no_record(gpu, oracle_lib, budget, monkeypatch):
     """UTTT_SELECT_BUDGET (in-place completions per tree and k_select launch) only spreads a move's

@@ -3167,7 +3167,9 @@ int uttt_search1_next(uttt_engine_t *e, uttt_state_t *leaf, int32_t *copies, int
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
         if (__atomic_load_n(&h->tag, __ATOMIC_ACQUIRE) == want) break;
-        if ((it & 255u) == 0u) {
+        // the stream is queried only for a wait past 20 ms (the wave's 100 ms timeout, a failed stream): a
+        // query goes through the runtime's locks (uttt_rounds_hash_move)
+        if ((it & 255u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
             const hipError_t q = hipStreamQuery(e->stream);
             if (q != hipSuccess && q != hipErrorNotReady) {
                 set_error("engine stream failed: %s", hipGetErrorString(q));
@@ -3450,6 +3452,64 @@ int uttt_rounds_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, flo
     for (int32_t i = 0; i < n_rounds; ++i)
         if (int rc = uttt_round_hash_async(e, (ring_slot + i) % kCountRing, tag + i, policy, value)) return rc;
     return UTTT_OK;
+}
+
+int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value, int32_t depth,
+                          int32_t *n_rounds, int64_t *n_leaves, int32_t *n_with_leaves) {
+    if (!e || !n_rounds || !n_leaves || !n_with_leaves || depth < 1 || depth >= kCountRing || ring_slot < 0 ||
+        ring_slot >= kCountRing) {
+        set_error("uttt_rounds_hash_move: bad arguments (depth in 1..%d, ring slot in 0..%d)", kCountRing - 1,
+                  kCountRing - 1);
+        return UTTT_ERR_ARG;
+    }
+    int32_t enq = 0, head = 0, with_leaves = 0;
+    int64_t leaves = 0;
+    auto tag_of = [tag](int32_t i) { return (int32_t)(((uint32_t)tag + (uint32_t)i) & 0x7FFFFFFFu); };
+    auto push = [&]() -> int {
+        const int rc = uttt_round_hash_async(e, (ring_slot + enq) % kCountRing, tag_of(enq), policy, value);
+        if (rc == UTTT_OK) ++enq;
+        return rc;
+    };
+    auto finish = [&](int rc) {
+        *n_rounds = enq;
+        *n_leaves = leaves;
+        *n_with_leaves = with_leaves;
+        return rc;
+    };
+    for (int32_t i = 0; i < depth; ++i)
+        if (int rc = push()) return finish(rc);
+    for (;;) {
+        const int32_t *w = e->h_ring + 4 * ((ring_slot + head) % kCountRing);
+        const int32_t want = tag_of(head);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned it = 1; __atomic_load_n(w + 3, __ATOMIC_ACQUIRE) != want; ++it) {
+            // the stream is queried only for a wait past 20 ms (a failed or finished stream): a query while the
+            // rounds run goes through the runtime's locks and cost tree-only self-play 7% when made every
+            // ~40 us (round 6)
+            if ((it & 1023u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
+                const hipError_t q = hipStreamQuery(e->stream);
+                if (q != hipSuccess && q != hipErrorNotReady) {
+                    set_error("engine stream failed: %s", hipGetErrorString(q));
+                    return finish(UTTT_ERR_HIP);
+                }
+                if (q == hipSuccess && __atomic_load_n(w + 3, __ATOMIC_ACQUIRE) != want) {
+                    set_error("engine: a hash round ended without storing its counts");
+                    return finish(UTTT_ERR_HIP);
+                }
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                    set_error("engine: a hash round's counts not stored within 60 s");
+                    return finish(UTTT_ERR_HIP);
+                }
+            }
+            __builtin_ia32_pause();
+        }
+        const int32_t n = __atomic_load_n(w + 0, __ATOMIC_ACQUIRE), left = __atomic_load_n(w + 2, __ATOMIC_ACQUIRE);
+        leaves += n;
+        with_leaves += n > 0 ? 1 : 0;
+        ++head;
+        if (left <= 0) return finish(UTTT_OK);  // the move's last round: the ones behind it are empty
+        if (int rc = push()) return finish(rc);
+    }
 }
 
 int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value) {

@@ -85,6 +85,7 @@ SIGNATURES = {
     "uttt_eval_hash_dev": (ctypes.c_int, [_P, _P, _P]),
     "uttt_round_hash_async": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "uttt_rounds_hash_async": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32]),
+    "uttt_rounds_hash_move": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, _P]),
     "uttt_search_select_host": (ctypes.c_int, [_P, _P, _P, _P]),
     "uttt_search_apply_host": (ctypes.c_int, [_P, _P, ctypes.c_int64, _P, ctypes.c_int32]),
     "uttt_search_root_visits": (ctypes.c_int, [_P, _I32P, _I32P]),

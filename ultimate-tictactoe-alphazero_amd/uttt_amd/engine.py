@@ -198,6 +198,21 @@ class Engine:
         self.n_pending = None
         return self.tag
 
+    def rounds_hash_move(self, ring_slot, policy, value, depth):
+        """A move's whole hash-round loop in one call (uttt_rounds_hash_move): `depth` rounds in flight from ring
+        slot ring_slot on, until a round leaves no tree with simulations. Returns (rounds enqueued, leaves,
+        rounds with leaves); the rounds' ring slots and tags are consumed (self.tag is the last one)."""
+        first = self._next_tag()
+        nr, nl, nz = ctypes.c_int32(0), ctypes.c_int64(0), ctypes.c_int32(0)
+        rc = self.lib.uttt_rounds_hash_move(self.h, int(ring_slot), first, ctypes.c_void_p(policy.data_ptr()),
+                                            ctypes.c_void_p(value.data_ptr()), int(depth), ctypes.byref(nr),
+                                            ctypes.byref(nl), ctypes.byref(nz))
+        if nr.value:
+            self.tag = (first + nr.value - 1) & 0x7FFFFFFF
+        check(rc)
+        self.n_pending = None
+        return nr.value, nl.value, nz.value
+
     def round_hash_async(self, ring_slot, policy, value):
         """A whole round with the hash evaluator in one call (uttt_round_hash_async): select, scan (the counts
         and then a new tag into ring slot ring_slot), hash evaluation of the pending leaves, apply. Returns

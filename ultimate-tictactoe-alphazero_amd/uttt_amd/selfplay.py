@@ -61,6 +61,11 @@ class HashEvaluator:
             return engine.round_hash_async(slot, self.policy, self.value)
         return engine.rounds_hash_async(slot, self.policy, self.value, self.rounds_per_call)
 
+    def round_move(self, engine, slot, depth):
+        """A move's whole round loop in one C call (Engine.rounds_hash_move): `depth` rounds in flight, the
+        host spinning on their tags in C, until a round leaves no tree with simulations."""
+        return engine.rounds_hash_move(slot, self.policy, self.value, depth)
+
 
 class NetworkEvaluator:
     """DualNetwork (or any model with its call signature) on the engine's device."""
@@ -118,8 +123,8 @@ class BatchedSearch:
 
 
 class _TagReady:
-    """Readiness of a one-call round: its ring slot's word 3 holds the round's tag (stored by k_scan after
-    the counts, a system-scope release), polled like an event."""
+    """Readiness of a one-call round: its ring slot's word 3 holds the round's tag (stored by k_scan or k_round1
+    after the counts, which are drained first), polled like an event."""
     __slots__ = ("buf", "tag")
 
     def __init__(self, buf, tag):
@@ -321,6 +326,10 @@ class SelfPlay:
                     progress(self.finished, None)
             return total
         depth = self._lookahead()
+        if (len(self.lanes) == 1 and depth > 1 and os.environ.get("UTTT_MOVE_LOOP", "1") != "0"
+                and getattr(self.lanes[0].evaluator, "round_move", None) is not None
+                and getattr(self.lanes[0].evaluator, "rounds_per_call", 1) == 1):
+            return self._steps_move_loop(self.lanes[0], k, depth, progress)
         spin = depth > 1 and os.environ.get("UTTT_POLL_SLEEP", "0") != "1"
         for ln in self.lanes:
             if ln.count_ring is None:
@@ -420,6 +429,54 @@ class SelfPlay:
                 if progress:
                     progress(self.finished, None)
         self.moves += moves / len(self.lanes)
+        self.sims += total
+        return total
+
+    def _steps_move_loop(self, ln, k, depth, progress):
+        """steps() for one lane whose evaluator runs a move's rounds in one C call (HashEvaluator.round_move,
+        round 6: tree-only self-play was bound by the host's per-round Python; UTTT_MOVE_LOOP=0 keeps the
+        Python round loop). Per move: the round loop in C (`depth` rounds in flight, spinning on their tags),
+        then the move's end and the next move's roots enqueued without waiting; the previous move's counters
+        are read once the next move's first count has landed (its end ran before it on the stream). Same
+        rounds, records and totals as the Python loop."""
+        e = ln.engine
+        if ln.count_ring is None:
+            ln.count_ring = e.count_ring()
+        with self._ctx(ln):
+            live = e.move_begin()  # the first move of the call: blocking, gives the live count
+        if live <= 0:
+            return 0
+        ln.cur_live = live
+        total = moves = 0
+        pending = False  # a move's end enqueued whose counters were not read yet
+        while k is None or moves < k:
+            n_rounds, leaves, with_leaves = ln.evaluator.round_move(e, ln.ring_pos % len(ln.count_ring), depth)
+            ln.ring_pos += n_rounds
+            if pending:  # the previous move's end ran before this move's first round
+                ln.finished, ln.cur_live = e.move_result()
+                pending = False
+                if progress:
+                    progress(self.finished, None)
+            if ln.cur_live == 0:  # every game of the lane is over: this move was empty
+                break
+            ln.leaves += leaves
+            ln.rounds += with_leaves
+            total += ln.cur_live * self.evaluate_count
+            moves += 1
+            e.move_end_async()
+            pending = True
+            if k is not None and moves == k:
+                break
+            e.move_begin_async()
+        if pending:
+            with self._ctx(ln):
+                ev = torch.cuda.Event()
+                ev.record()
+            ev.synchronize()
+            ln.finished, ln.cur_live = e.move_result()
+            if progress:
+                progress(self.finished, None)
+        self.moves += moves
         self.sims += total
         return total
 
