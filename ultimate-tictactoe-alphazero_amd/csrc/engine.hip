@@ -432,8 +432,22 @@ __device__ bool cache_lookup_probed(const EvalCache &c, const CacheProbe &pr, co
 // expand_backup computed it) valid: it is stored beside the values (value 82, with 1.0f at 83), so a
 // hit expands without re-adding up to 81 priors one dependent add after another.
 constexpr int kRecSum = 82, kRecSumFlag = 83;
-__device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0, float p1, float v, bool has_sum = false,
-                             float psum = 0.0f) {
+// A publish held back by cache_insert (defer): the claimed slot and its flag value, stored by the caller once
+// its own later stores are drained anyway (k_round1's end of block), so the record's drain is not a round
+// trip of its own on the wave's chain (round 6)
+struct CachePublish {
+    int32_t slot;  // -1: nothing held
+    uint32_t pub;
+};
+__device__ __forceinline__ void cache_publish(const EvalCache &c, const CachePublish &d) {
+    if (d.slot < 0 || (threadIdx.x & 63) != 0) return;
+    st_agent(c.flag + d.slot, d.pub);
+    atomicAdd(stripe_of(c.ctr + 2 * kRow), 1ull);
+}
+
+// pr: the kProbe slots' flags for s, loaded ahead (cache_probe_issue, before the expansion's work)
+__device__ bool cache_insert(const EvalCache &c, const CacheProbe &pr, const uttt_state_t &s, float p0, float p1, float v,
+                             bool has_sum = false, float psum = 0.0f, CachePublish *defer = nullptr) {
     if (!c.flag) return false;
     const int lane = (int)(threadIdx.x & 63);
     int slot = -1;
@@ -441,9 +455,9 @@ __device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
     // the kProbe slots' flags in one round trip (lanes 0..kProbe-1), then lane 0 acts on the first
     // slot that holds this position's tag or is empty; a lost claim falls back to probing one slot
     // after another from there
-    const uint64_t h64 = state_hash64(s);
+    const uint64_t h64 = pr.h64;
     const uint32_t h = (uint32_t)h64, tag = state_tag(h64);
-    const uint32_t f = lane < kProbe ? ld_agent(c.flag + ((h + (uint32_t)lane) & c.mask)) : 0u;
+    const uint32_t f = pr.f;
     const uint64_t here = __ballot(lane < kProbe && flag_ready(f) && flag_tag(f) == tag);
     const uint64_t free_ = __ballot(lane < kProbe && f == 0u);
     const uint64_t either = here | free_;
@@ -507,11 +521,13 @@ __device__ bool cache_insert(const EvalCache &c, const uttt_state_t &s, float p0
     // a partial-line write at the memory side (round 6; 23 pieces left the third line 112 of 128 bytes)
     if (lane < kRecBytes / 16)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, piece), r, 16 * lane, 0, kSc1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        st_agent(c.flag + slot, pub);
-        atomicAdd(stripe_of(c.ctr + 2 * kRow), 1ull);
+    if (defer) {  // the caller drains and publishes
+        defer->slot = slot;
+        defer->pub = pub;
+        return true;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cache_publish(c, CachePublish{slot, pub});
     return true;
 }
 
@@ -1321,7 +1337,7 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
                                            const int32_t *__restrict__ rowbase, int per_copy,
                                            unsigned long long *bytes_ctr, int slot, float *row /* LDS, 84 floats */,
                                            int by_tree = -1, int by_tree_depth = 0, float *copy_rows = nullptr,
-                                           bool host_rows = false) {
+                                           bool host_rows = false, CachePublish *defer = nullptr) {
     // copy_rows (LDS, 8 x 84 floats, 16-B aligned; optional): the per-copy prior sums of a chunk run in 8 lanes
     // at once instead of one copy after another. host_rows: the evaluation rows sit in fine-grained host
     // memory the host wrote behind a polled command; they are read with system-coherent (sc0 sc1) loads,
@@ -1411,6 +1427,8 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
             }
         }
         const bool cacheable = __ballot(!fin0 || (lane < 17 && !fin1)) == 0ull;
+        // the insert's flag loads go out before the expansion's work, which runs under their round trip
+        const CacheProbe ipr = cache_probe_issue(cache, s);
         float psum = 0.0f;
         if (!expand_backup(pool, base, r.node, depth, pn_lo, pn_hi, pr_lo, pr_hi, k, s, raw0, lane < 17 ? raw1 : 0.0f,
                            v, ctl.node_count, tr.py != 0, row, false, 0.0f, &psum)) {
@@ -1420,7 +1438,7 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
             }
             return;
         }
-        inserted = cacheable && cache_insert(cache, s, raw0, raw1, v, tr.py == 0, psum);
+        inserted = cacheable && cache_insert(cache, ipr, s, raw0, raw1, v, tr.py == 0, psum, defer);
         L = (ctl.node_count - nodes_before) / k;
     } else {
         // the reference's exact call pattern: k results, one per queued copy, applied in order
@@ -1663,11 +1681,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
     const int lane = lane_id();
     if (threadIdx.x == 0) s_cnt = 0u;
     __syncthreads();
+    CachePublish held{-1, 0u};  // the apply's cache insert, published after this block's drain below
     if (t < tr.n_trees) {
         const int prev = __builtin_amdgcn_readfirstlane(tr.pending[t]);  // the previous round's, until the select
         if (apply && (prev & 1)) {
             apply_wave(pool, tr, cache, apply_policy, 81, apply_value, 1, nullptr, 0,
-                       stats ? stats + kKApply * kRow : nullptr, t, s_row[threadIdx.x >> 6], t, prev >> 8);
+                       stats ? stats + kKApply * kRow : nullptr, t, s_row[threadIdx.x >> 6], t, prev >> 8, nullptr,
+                       false, &held);
             wave_memory_fence();  // the descent reads the records the apply wrote
         }
         const int p = select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0);
@@ -1681,8 +1701,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
             atomicAdd(&s_cnt, (uint32_t)((q == 1 || q == 3) ? 1 : 0) | ((q == 2 ? 1u : 0u) << 10) |
                                   ((q >= 2 ? 1u : 0u) << 20));
     }
-    // every wave's stores (rows, records, stats atomics) complete before the block's partial is published
+    // every wave's stores (rows, records, stats atomics, a held cache record) complete before the block's
+    // partial is published, and before the held record's flag
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    cache_publish(cache, held);
     __syncthreads();
     const int nb = (int)gridDim.x, b = (int)blockIdx.x;
     if (threadIdx.x == 0) {
