@@ -3613,7 +3613,12 @@ int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
         leaves += n;
         with_leaves += n > 0 ? 1 : 0;
         ++head;
-        if (left <= 0) return finish(UTTT_OK);  // the move's last round: the ones behind it are empty
+        if (left <= 0) {  // the move's last round: the ones behind it are empty
+            // a round enqueued behind it applied its leaves and queued none, so the evaluation staged by the
+            // last enqueued round is empty: the move end need not flush it (one k_apply_tree launch less)
+            if (enq > head) e->dev_apply_staged = false;
+            return finish(UTTT_OK);
+        }
         if (int rc = push()) return finish(rc);
     }
 }
