@@ -18,6 +18,13 @@ from conftest import GOLDEN, PKG, REPO, golden
 pytestmark = pytest.mark.gpu
 
 
+def _failure_text(r):
+    """A child run's failure: its error lines first (a C++ exception's message sits above the stack trace
+    that the tails would keep), then the tails."""
+    err = [ln for ln in r.stderr.splitlines() if "rror" in ln and "frame #" not in ln][:12]
+    return "\n".join(err) + "\n---\n" + r.stdout[-2000:] + r.stderr[-3000:]
+
+
 @pytest.fixture(scope="module")
 def gpu():
     import torch
@@ -134,7 +141,7 @@ def test_self_play_cpp_sharded_over_two_ranks(gpu, tmp_path):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(REPO, "tests", "sharded_selfplay_main.py"), str(tmp_path), str(ng), str(int(d["seeds"][0]))]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, cwd=REPO)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.returncode == 0, _failure_text(r)
     files = sorted(p for p in os.listdir(tmp_path) if p.endswith(".history"))
     assert len(files) == 1, files
     with open(os.path.join(tmp_path, files[0]), "rb") as fh:
@@ -152,7 +159,7 @@ def test_rccl_one_rank_data_path_and_ddp(gpu):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(REPO, "tests", "rccl_one_rank_main.py")]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, cwd=REPO)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.returncode == 0, _failure_text(r)
     assert "RCCL-OK" in r.stdout
 
 
@@ -167,7 +174,7 @@ def test_flat_dp_train_network_two_ranks(gpu, tmp_path):
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(REPO, "tests", "dp_flat_two_ranks_main.py"), str(tmp_path)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, cwd=REPO)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.returncode == 0, _failure_text(r)
     m0 = torch.load(tmp_path / "m0.pt", weights_only=True)
     m1 = torch.load(tmp_path / "m1.pt", weights_only=True)
     for k in m0["sd"]:
@@ -185,7 +192,7 @@ def test_bench_multi_rank_path(gpu):
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--age", "3", "--games", "256",
            "--rehearse-shared-gpu", "--no-variants", "--no-cpu-baseline"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.returncode == 0, _failure_text(r)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])

@@ -3929,11 +3929,6 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
     HIP_TRY(hipSetDevice(e->device));
     if (int rc0 = flush_host_apply(e)) return rc0;  // a staged round's evaluation (uttt_round_hash_async)
     if (int rc0 = join_seed(e)) return rc0;         // the previous move end's key seeding
-    if (!e->seed_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&e->seed_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_fin, hipEventDisableTiming | hipEventDisableSystemFence));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_seed, hipEventDisableTiming | hipEventDisableSystemFence));
-    }
     const int slots = e->sp.slots;
     {  // d_err was reset by this move's k_begin
         TimedLaunch tl(e, kKMoveEnd);
@@ -3952,6 +3947,11 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
             return v && v[0] == '1';
         }();
         if (side) {
+            if (!e->seed_stream) {
+                HIP_TRY(hipStreamCreateWithFlags(&e->seed_stream, hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&e->ev_fin, hipEventDisableTiming | hipEventDisableSystemFence));
+                HIP_TRY(hipEventCreateWithFlags(&e->ev_seed, hipEventDisableTiming | hipEventDisableSystemFence));
+            }
             HIP_TRY(hipEventRecord(e->ev_fin, e->stream));
             HIP_TRY(hipStreamWaitEvent(e->seed_stream, e->ev_fin, 0));
             hipLaunchKernelGGL(k_seed, dim3(archive_grid(slots)), dim3(kWave), 0, e->seed_stream, e->sp, err);
