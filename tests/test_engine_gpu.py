@@ -191,13 +191,14 @@ def test_move_loop_in_c_equals_the_python_round_loop(gpu, oracle_lib, monkeypatc
     """One lane with the hash evaluator runs each move's round loop in one C call (uttt_rounds_hash_move,
     SelfPlay._steps_move_loop); UTTT_MOVE_LOOP=0 keeps the Python round loop. Both give the oracle's records,
     the same totals (simulations, rounds with leaves, leaves, finished games) and play the same moves per
-    steps(k) call."""
+    steps(k) call. The evaluation cache is off here: with it on, whether a tree hits a position another tree
+    inserts in the same round depends on timing, which moves leaves between rounds (never a record)."""
     n_games, seed = 20, 909
     ref = [oracle_lib.self_play_game_hash(seed + g, 1.0, 30, 4) for g in range(n_games)]
     stats = {}
     for loop in ("1", "0"):
         monkeypatch.setenv("UTTT_MOVE_LOOP", loop)
-        sp = gpu.SelfPlay(6, 30, 4, 1.0)
+        sp = gpu.SelfPlay(6, 30, 4, 1.0, cache_log2=0)
         sp.begin(0, n_games, seed)
         per_call = [sp.steps(5) for _ in range(3)]
         per_call.append(sp.steps())

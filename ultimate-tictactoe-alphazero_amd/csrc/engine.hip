@@ -157,6 +157,9 @@ struct Trees {
     int32_t py;  // 1: pv_mcts.py semantics (arena), 0: cpp/uttt_mcts.cpp (self-play)
     int32_t budget;  // in-place completions per tree and select launch (kSelectBudget; UTTT_SELECT_BUDGET)
 };
+// count[3]: nonzero once any tree of the search has failed (reset by k_begin): the asynchronous move end reads
+// it instead of a launch that scans every tree's status (k_finalize finds the first failed tree only then)
+__device__ __forceinline__ void flag_tree_error(const Trees &tr) { atomicOr(tr.count + 3, 1); }
 
 // record packing (Pool)
 constexpr uint32_t kNoAction = 0x7Fu;
@@ -673,8 +676,9 @@ __device__ bool expand_backup(const Pool &pool, size_t base, int node, int depth
 // ----------------------------------------------------------- root (begin) --
 // uttt_mcts.cpp:92-103: root expanded at once with uniform priors 1.0f/|legal|.
 // Self-play passes `live` (slot flags) and the slots' states in place (src_stride = sizeof(Slot)),
-// and err: the asynchronous move end's failure word, reset here (once per move, before this move's
-// k_tree_err, after the previous move end's read of it) instead of by a memset on the stream;
+// and err: the asynchronous move end's failure word, reset here (once per move, before this move's end,
+// after the previous move end's read of it) instead of by a memset on the stream, as is the search's
+// failure flag (Trees::count[3]);
 // search passes nullptr (all live) and packed states.
 __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const char *src, int src_stride, const int32_t *live,
                                                   unsigned long long *err) {
@@ -683,6 +687,7 @@ __global__ __launch_bounds__(kBlock) void k_begin(Pool pool, Trees tr, const cha
     if (t == 0 && lane == 0) {
         if (err) *err = ~0ull;
         tr.count[2] = -1;  // a search starts: no round of it is known to be empty yet (k_round1's fast exit)
+        tr.count[3] = 0;   // and no tree of it has failed
     }
     if (t >= tr.n_trees) return;
     const bool on = live ? (live[t] != 0) : true;
@@ -990,14 +995,20 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                 bytes += 12ull * (unsigned long long)cnt + 8ull;
                 if (bi == kNone) {  // every child NaN: the reference would dereference null
                     fail = true;
-                    if (lane == 0) ctl.status |= kErrSelect;
+                    if (lane == 0) {
+                        ctl.status |= kErrSelect;
+                        flag_tree_error(tr);
+                    }
                     break;
                 }
                 node = first + bi;
                 ++depth;
                 if (depth >= kMaxDepth) {
                     fail = true;
-                    if (lane == 0) ctl.status |= kErrDepth;
+                    if (lane == 0) {
+                        ctl.status |= kErrDepth;
+                        flag_tree_error(tr);
+                    }
                     break;
                 }
                 if (PY) {
@@ -1070,7 +1081,10 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                 const bool hs = !PY && cv[kRecSumFlag] == 1.0f;
                 if (!expand_backup(pool, base, node, depth, path_lo, path_hi, prec_lo, prec_hi, k, s, h0, h1, hv,
                                    ctl.node_count, PY, cv, hs, cv[kRecSum], nullptr, &root_rec)) {
-                    if (lane == 0) ctl.status |= kErrCapacity;
+                    if (lane == 0) {
+                        ctl.status |= kErrCapacity;
+                        flag_tree_error(tr);
+                    }
                     break;
                 }
                 root_known = true;
@@ -1422,6 +1436,7 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
                 if (lane == 0) {
                     ctl.status |= kErrNonFinite;
                     tr.ctl[t] = ctl;
+                    flag_tree_error(tr);
                 }
                 return;
             }
@@ -1435,6 +1450,7 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
+                flag_tree_error(tr);
             }
             return;
         }
@@ -1455,6 +1471,7 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
             if (lane == 0) {
                 ctl.status |= kErrCapacity;
                 tr.ctl[t] = ctl;
+                flag_tree_error(tr);
             }
             return;
         }
@@ -1525,6 +1542,7 @@ __device__ __forceinline__ void apply_wave(Pool pool, Trees tr, EvalCache cache,
             if (lane == 0) {
                 ctl.status |= kErrNonFinite;
                 tr.ctl[t] = ctl;
+                flag_tree_error(tr);
             }
             return;
         }
@@ -2196,15 +2214,6 @@ __device__ double np_sum(const double *a, int n, int stride) {
     return res;  // n <= 81 < 128: a single pairwise block
 }
 
-// The asynchronous move end's failure check: the first failed tree (lowest slot) and its status
-// into *err (~0 = none), read by the move-end kernels behind it on the stream and by the host.
-__global__ __launch_bounds__(256) void k_tree_err(const TreeCtl *__restrict__ ctl, int n, unsigned long long *err) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const uint32_t st = (uint32_t)ctl[s].status;
-    if (st & kErrMask) atomicMin(err, ((unsigned long long)s << 32) | st);
-}
-
 // A double held by lane i of the wave (i uniform), to every lane: the sequential f64 sums below run
 // the reference's additions in its order on values spread over the lanes, without an LDS round trip.
 __device__ __forceinline__ double lane_double(double x, int i) {
@@ -2226,21 +2235,21 @@ __device__ __forceinline__ double row_entry(double x0, double x1, int i) {
 // integer visit counts) is a wave reduction, what is not (np.sum's pairwise blocks, the cumsum of
 // np.random.choice) runs the reference's additions in its order on readlane operands, the same in
 // every lane. Round 3's thread-per-slot form walked the row in LDS, 81-step dependent chains per pass.
-__global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, const unsigned long long *err) {
-    // asynchronous form: k_tree_err has folded the failed trees into *err; on a failure this move's
-    // end changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
+// fail (the asynchronous form: the search's failure flag, Trees::count[3]): on a failure this move's end
+// changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
+__global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, const int32_t *fail) {
     const int lane = lane_id();
     const int s = wave_index();
     if (s >= sp.slots) return;
     // the loads that do not depend on each other are issued together (round 6: the failure word, the slot,
     // the key position and the root's record were four dependent round trips before the first draw)
     const size_t base = (size_t)s * pool.cap;
-    const unsigned long long ev = err ? *err : ~0ull;
+    const int32_t failed = fail ? *fail : 0;
     Slot sl = sp.slot[s];
     int32_t pos = sp.mt_pos[s];
     int first;
     const int L = root_children(pool, base, first);
-    if (ev != ~0ull) return;
+    if (failed) return;
     sl.finished = 0;
     if (!sl.live) {
         if (lane == 0) sp.slot[s] = sl;
@@ -2383,11 +2392,27 @@ __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, con
 __device__ __forceinline__ void store_host_i64(int64_t *p, int64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const unsigned long long *err, int64_t *host_move) {
+// fail / ctl / err (the asynchronous form): when the search's failure flag is set, the first failed tree
+// (lowest slot) and its status go to *err (k_archive skips then) and to host_move[4], and the move is not
+// ended (k_move_end changed nothing); the status scan runs only on that rare path (round 6: a k_tree_err
+// launch per move scanned every tree's status on the critical path)
+__global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const int32_t *fail, const TreeCtl *ctl,
+                                                   unsigned long long *err, int64_t *host_move) {
     __shared__ unsigned long long wsum[32];
     __shared__ int s_work;  // entries of k_archive's work list
-    if (err && *err != ~0ull) {  // a failed tree: the move is not ended (k_move_end)
-        if (host_move && threadIdx.x == 0) store_host_i64(host_move + 4, (int64_t)*err);
+    __shared__ unsigned long long s_first;
+    if (fail && *fail) {
+        if (threadIdx.x == 0) s_first = ~0ull;
+        __syncthreads();
+        for (int t = threadIdx.x; t < sp.slots; t += blockDim.x) {
+            const uint32_t st = (uint32_t)ctl[t].status;
+            if (st & kErrMask) atomicMin(&s_first, ((unsigned long long)t << 32) | st);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            *err = s_first;
+            if (host_move) store_host_i64(host_move + 4, (int64_t)s_first);
+        }
         return;
     }
     const int tid = threadIdx.x;
@@ -3806,8 +3831,8 @@ int uttt_selfplay_begin(uttt_engine_t *e, int64_t game_begin, int64_t game_end, 
     HIP_TRY(hipMemsetAsync(sp.slot, 0, sizeof(Slot) * slots, e->stream));
     int64_t ctr[4] = {game_begin, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(sp.ctr, ctr, sizeof(ctr), hipMemcpyHostToDevice, e->stream));
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const unsigned long long *)nullptr,
-                       (int64_t *)nullptr);
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, sp, (const int32_t *)nullptr,
+                       (const TreeCtl *)nullptr, (unsigned long long *)nullptr, (int64_t *)nullptr);
     hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, sp, (const unsigned long long *)nullptr, 1);
     if ((rc = check_launch())) return rc;
     HIP_TRY(hipMemcpyAsync(e->h_move, sp.ctr, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, e->stream));
@@ -3870,8 +3895,10 @@ int uttt_selfplay_move_end(uttt_engine_t *e, int64_t *n_finished) {
     {
         TimedLaunch tl(e, kKMoveEnd);
         const unsigned long long *no_err = nullptr;
-        hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, no_err);
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, no_err, (int64_t *)nullptr);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream,
+                           e->pool, e->sp, (const int32_t *)nullptr);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, (const int32_t *)nullptr,
+                           (const TreeCtl *)nullptr, (unsigned long long *)nullptr, (int64_t *)nullptr);
         hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, e->sp, no_err, 1);
     }
     if ((rc = check_launch())) return rc;
@@ -3930,15 +3957,17 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
     if (int rc0 = flush_host_apply(e)) return rc0;  // a staged round's evaluation (uttt_round_hash_async)
     if (int rc0 = join_seed(e)) return rc0;         // the previous move end's key seeding
     const int slots = e->sp.slots;
-    {  // d_err was reset by this move's k_begin
+    {  // d_err and the failure flag were reset by this move's k_begin
         TimedLaunch tl(e, kKMoveEnd);
-        // a failed tree leaves the whole move unended (k_tree_err -> *d_err; the kernels behind it
-        // check it), so the engine is in the state the blocking move end refuses in
-        hipLaunchKernelGGL(k_tree_err, dim3((slots + 255) / 256), dim3(256), 0, e->stream, (const TreeCtl *)e->tr.ctl,
-                           slots, e->d_err);
+        // a failed tree leaves the whole move unended (the failure flag, set where a tree's status gets an
+        // error bit; k_finalize then puts the first failed tree into *d_err, which k_archive checks), so the
+        // engine is in the state the blocking move end refuses in
+        const int32_t *fail = e->tr.count + 3;
         const unsigned long long *err = e->d_err;
-        hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream, e->pool, e->sp, err);
-        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, err, e->h_move);
+        hipLaunchKernelGGL(k_move_end, dim3((slots + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, e->stream,
+                           e->pool, e->sp, fail);
+        hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, fail, (const TreeCtl *)e->tr.ctl,
+                           e->d_err, e->h_move);
         // UTTT_SEED_STREAM=1: the refilled slots' keys are seeded on a side stream, overlapping the archive copy
         // and the next move's rounds, and the next move end joins it (round 6, measured: tree-only +1.3% with
         // the seed chain at 18 us, headline within noise; after the chain's rewrite k_archive seeds in place)
