@@ -834,8 +834,9 @@ def test_nonfinite_evaluator_output_is_refused(gpu, oracle_lib):
 
 def test_nonfinite_in_async_selfplay_leaves_the_move_unended(gpu, oracle_lib):
     """Self-play with device-count rounds and asynchronous move ends: a NaN value stops its tree,
-    the move end that follows changes nothing (k_tree_err, then k_move_end / k_finalize / k_archive
-    skip), and the host raises UTTT_ERR_NONFINITE when it reads that move's result. Every game
+    the move end that follows changes nothing (the search's failure flag: k_move_end / k_finalize /
+    k_archive skip, k_finalize records the first failed tree), and the host raises UTTT_ERR_NONFINITE when it
+    reads that move's result. Every game
     archived before the failure equals the oracle's."""
     import torch
     from uttt_amd._lib import EngineError
