@@ -1672,20 +1672,48 @@ __device__ __forceinline__ void hash_leaf_row(const uttt_state_t &s, float *__re
 // counters for the next round. Every tree's work is k_round's in the same order, so every result is the
 // three-dispatch round's (the fused-rounds test runs both).
 constexpr int kR1Stripes = 8;
+// uttt_rounds_hash_move's per-block count words: n0 (queued leaves) bits 0-4, n1 (budget stops) 5-9, n2
+// (trees with simulations left) 10-14, at most kWavesPerBlock = 16 each; the round's tag (17 bits) above
+constexpr int kPartTagShift = 15;
+constexpr uint32_t kPartTagMask = 0x1FFFFu;
+constexpr uint32_t kPartLiveMask = 0x1Fu | (0x1Fu << 10);
+static_assert(kWavesPerBlock <= 31, "k_round1's per-block count words hold 5-bit counts");
 constexpr int kR1Partial = 64;  // rctl: [0..7] stripe arrivals, [32] top, [64 + block] partials
 template <bool PY>
 __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalCache cache, const float *apply_policy,
                                                    const float *apply_value, float *__restrict__ policy,
                                                    float *__restrict__ value, int apply, unsigned long long *stats,
-                                                   int32_t *host_count, int32_t tag, uint32_t *rctl) {
+                                                   int32_t *host_count, int32_t tag, uint32_t *rctl,
+                                                   uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev,
+                                                   int nb_prev) {
     __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];
     __shared__ uint32_t s_cnt;
     __shared__ int s_last;
+    // part_host (uttt_rounds_hash_move's rounds, no kernel timing): no last-block publish. Each block stores its
+    // counts with the round's tag into its own word of a host array (and of a device array the next round's
+    // empty-round check reads, part_prev), and the host sums the words once every block's has the tag: the
+    // arrival atomics, the partials' reload and the last block's drain left each round's critical path (round 6)
+    if (part_host) {
+        const uint32_t t17 = ((uint32_t)tag & kPartTagMask) << kPartTagShift;
+        bool empty = false;
+        if (part_prev) {  // the previous round queued no leaf and left no tree with simulations
+            bool busy = false;
+            for (int i = threadIdx.x; i < nb_prev; i += kBlock) busy |= (part_prev[i] & kPartLiveMask) != 0u;
+            empty = !__syncthreads_or(busy);
+        }
+        if (empty) {
+            if (threadIdx.x == 0) {
+                part_dev[blockIdx.x] = t17;
+                __hip_atomic_store(part_host + blockIdx.x, t17, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
+    }
     // a round behind one that queued no leaf and left no tree with simulations (the host's look-ahead rounds
     // past a move's end) has nothing to apply or select: every pending word is already 0 and the counts
     // stay 0, so block 0 publishes them and its tag, and every other block leaves at once (round 6: such a
     // round cost ~19 us of GPU time as a full pass over the trees; k_begin marks a new search non-empty)
-    if (tr.count[0] == 0 && tr.count[2] == 0) {
+    if (!part_host && tr.count[0] == 0 && tr.count[2] == 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0 && host_count) {
             st_host(host_count + 0, 0);
             st_host(host_count + 1, 0);
@@ -1724,6 +1752,15 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     cache_publish(cache, held);
     __syncthreads();
+    if (part_host) {  // the block's counts and the round's tag, one word (its stores drained above)
+        if (threadIdx.x == 0) {
+            const uint32_t w = (((uint32_t)tag & kPartTagMask) << kPartTagShift) | ((s_cnt >> 20) << 10) |
+                               (((s_cnt >> 10) & 0x3FFu) << 5) | (s_cnt & 0x3FFu);
+            part_dev[blockIdx.x] = w;
+            __hip_atomic_store(part_host + blockIdx.x, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     const int nb = (int)gridDim.x, b = (int)blockIdx.x;
     if (threadIdx.x == 0) {
         __hip_atomic_store(rctl + kR1Partial + b, s_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2660,6 +2697,10 @@ struct uttt_engine {
     uttt_state_t s1_root{};
     float s1_temperature = 0.0f;
     uint32_t *d_r1ctl = nullptr;     // k_round1's arrival counters and per-block partials (zero between rounds)
+    // uttt_rounds_hash_move's per-block count words: host [kCountRing][part_cap] (fine-grained pinned), device
+    // [2][part_cap] (the previous round's, for the empty-round check)
+    uint32_t *h_part = nullptr, *d_part = nullptr;
+    int32_t part_cap = 0;
     int32_t host_apply_rows = 0;  // a one-tree evaluation staged by uttt_search_apply_host, applied by the next
                                   // k_flush1 (or by flush_host_apply before any other call that reads the tree)
     int32_t leaf_tag = 0;
@@ -2959,6 +3000,7 @@ int uttt_engine_destroy(uttt_engine_t *e) {
     }
     if (e->h_count) (void)hipHostFree(e->h_count);
     if (e->h_ring) (void)hipHostFree(e->h_ring);
+    if (e->h_part) (void)hipHostFree(e->h_part);
     if (e->h_leaf) (void)hipHostFree(e->h_leaf);
     if (e->h_eval) (void)hipHostFree(e->h_eval);
     if (e->h_s1) (void)hipHostFree(e->h_s1);
@@ -3585,6 +3627,17 @@ int uttt_rounds_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, flo
     return UTTT_OK;
 }
 
+static int round_hash_async_impl(uttt_engine *e, int32_t ring_slot, int32_t tag, float *policy, float *value,
+                                 uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev, int nb_prev);
+
+static bool one_dispatch_rounds() {  // k_round1 (UTTT_ROUND_DISPATCHES=3 / UTTT_FUSED_ROUNDS=0: the round-5 forms)
+    static const bool one = [] {
+        const char *f = getenv("UTTT_FUSED_ROUNDS"), *d = getenv("UTTT_ROUND_DISPATCHES");
+        return !(f && f[0] == '0') && !(d && d[0] == '3');
+    }();
+    return one;
+}
+
 int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value, int32_t depth,
                           int32_t *n_rounds, int64_t *n_leaves, int32_t *n_with_leaves) {
     if (!e || !n_rounds || !n_leaves || !n_with_leaves || depth < 1 || depth >= kCountRing || ring_slot < 0 ||
@@ -3593,11 +3646,35 @@ int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
                   kCountRing - 1);
         return UTTT_ERR_ARG;
     }
+    // per-block count words (k_round1's part_host form: no last-block publish; UTTT_ROUND_PARTS=0 keeps the ring
+    // slot's counts); not with kernel timing, whose select statistics the last block folds
+    static const bool parts_env = [] {
+        const char *v = getenv("UTTT_ROUND_PARTS");
+        return !(v && v[0] == '0');
+    }();
+    const bool parts = parts_env && one_dispatch_rounds() && !e->timing;
+    const int nb = grid_waves(e->tr.n_trees);
+    if (parts && !e->h_part) {
+        const int cap = grid_waves(e->max_trees);
+        if (hipHostMalloc((void **)&e->h_part, sizeof(uint32_t) * (size_t)kCountRing * cap, hipHostMallocCoherent) !=
+            hipSuccess) {
+            set_error("hipHostMalloc failed");
+            return UTTT_ERR_HIP;
+        }
+        memset(e->h_part, 0xFF, sizeof(uint32_t) * (size_t)kCountRing * cap);  // no word valid (n0 field 31)
+        if (int rc = alloc_n(e, &e->d_part, (size_t)2 * cap)) return rc;
+        e->part_cap = cap;
+    }
+    const int cap = e->part_cap;
     int32_t enq = 0, head = 0, with_leaves = 0;
     int64_t leaves = 0;
     auto tag_of = [tag](int32_t i) { return (int32_t)(((uint32_t)tag + (uint32_t)i) & 0x7FFFFFFFu); };
     auto push = [&]() -> int {
-        const int rc = uttt_round_hash_async(e, (ring_slot + enq) % kCountRing, tag_of(enq), policy, value);
+        const int slot = (ring_slot + enq) % kCountRing;
+        const int rc = parts ? round_hash_async_impl(e, slot, tag_of(enq), policy, value, e->h_part + (size_t)slot * cap,
+                                                     e->d_part + (size_t)(enq & 1) * cap,
+                                                     enq ? e->d_part + (size_t)((enq - 1) & 1) * cap : nullptr, nb)
+                             : uttt_round_hash_async(e, slot, tag_of(enq), policy, value);
         if (rc == UTTT_OK) ++enq;
         return rc;
     };
@@ -3607,34 +3684,63 @@ int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
         *n_with_leaves = with_leaves;
         return rc;
     };
+    // the spin's failure checks: the stream is queried only for a wait past 20 ms (a failed or finished
+    // stream): a query while the rounds run goes through the runtime's locks and cost tree-only self-play 7%
+    // when made every ~40 us (round 6)
+    auto still_waiting = [&](const std::chrono::steady_clock::time_point &t0, unsigned it, auto &&ready) -> int {
+        if ((it & 1023u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                set_error("engine stream failed: %s", hipGetErrorString(q));
+                return UTTT_ERR_HIP;
+            }
+            if (q == hipSuccess && !ready()) {
+                set_error("engine: a hash round ended without storing its counts");
+                return UTTT_ERR_HIP;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+                set_error("engine: a hash round's counts not stored within 60 s");
+                return UTTT_ERR_HIP;
+            }
+        }
+        __builtin_ia32_pause();
+        return UTTT_OK;
+    };
     for (int32_t i = 0; i < depth; ++i)
         if (int rc = push()) return finish(rc);
     for (;;) {
-        const int32_t *w = e->h_ring + 4 * ((ring_slot + head) % kCountRing);
+        const int slot = (ring_slot + head) % kCountRing;
         const int32_t want = tag_of(head);
         const auto t0 = std::chrono::steady_clock::now();
-        for (unsigned it = 1; __atomic_load_n(w + 3, __ATOMIC_ACQUIRE) != want; ++it) {
-            // the stream is queried only for a wait past 20 ms (a failed or finished stream): a query while the
-            // rounds run goes through the runtime's locks and cost tree-only self-play 7% when made every
-            // ~40 us (round 6)
-            if ((it & 1023u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
-                const hipError_t q = hipStreamQuery(e->stream);
-                if (q != hipSuccess && q != hipErrorNotReady) {
-                    set_error("engine stream failed: %s", hipGetErrorString(q));
-                    return finish(UTTT_ERR_HIP);
-                }
-                if (q == hipSuccess && __atomic_load_n(w + 3, __ATOMIC_ACQUIRE) != want) {
-                    set_error("engine: a hash round ended without storing its counts");
-                    return finish(UTTT_ERR_HIP);
-                }
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
-                    set_error("engine: a hash round's counts not stored within 60 s");
-                    return finish(UTTT_ERR_HIP);
-                }
+        int32_t n = 0, left = 0;
+        if (parts) {  // every block's word carries this round's tag: sum them
+            const uint32_t *pw = e->h_part + (size_t)slot * cap;
+            const uint32_t want17 = (uint32_t)want & kPartTagMask;
+            auto word_ok = [&](uint32_t w) { return (w >> kPartTagShift) == want17 && (w & 0x1Fu) <= 16u; };
+            int i = 0;
+            auto all_ready = [&] {
+                for (int j = 0; j < nb; ++j)
+                    if (!word_ok(__atomic_load_n(pw + j, __ATOMIC_ACQUIRE))) return false;
+                return true;
+            };
+            for (unsigned it = 1; i < nb; ++it) {
+                while (i < nb && word_ok(__atomic_load_n(pw + i, __ATOMIC_ACQUIRE))) ++i;
+                if (i < nb)
+                    if (int rc = still_waiting(t0, it, all_ready)) return finish(rc);
             }
-            __builtin_ia32_pause();
+            for (int j = 0; j < nb; ++j) {
+                const uint32_t w = __atomic_load_n(pw + j, __ATOMIC_ACQUIRE);
+                n += (int32_t)(w & 0x1Fu);
+                left += (int32_t)((w >> 10) & 0x1Fu);
+            }
+        } else {
+            const int32_t *w = e->h_ring + 4 * slot;
+            auto ready = [&] { return __atomic_load_n(w + 3, __ATOMIC_ACQUIRE) == want; };
+            for (unsigned it = 1; !ready(); ++it)
+                if (int rc = still_waiting(t0, it, ready)) return finish(rc);
+            n = __atomic_load_n(w + 0, __ATOMIC_ACQUIRE);
+            left = __atomic_load_n(w + 2, __ATOMIC_ACQUIRE);
         }
-        const int32_t n = __atomic_load_n(w + 0, __ATOMIC_ACQUIRE), left = __atomic_load_n(w + 2, __ATOMIC_ACQUIRE);
         leaves += n;
         with_leaves += n > 0 ? 1 : 0;
         ++head;
@@ -3649,6 +3755,13 @@ int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
 }
 
 int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, float *policy, float *value) {
+    return round_hash_async_impl(e, ring_slot, tag, policy, value, nullptr, nullptr, nullptr, 0);
+}
+
+// part_host != nullptr (uttt_rounds_hash_move only, with the one-dispatch rounds and no kernel timing): the
+// round's counts go to per-block words instead of the ring slot (k_round1's part_host form)
+static int round_hash_async_impl(uttt_engine *e, int32_t ring_slot, int32_t tag, float *policy, float *value,
+                                 uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev, int nb_prev) {
     if (!e || !policy || !value || ring_slot < 0 || ring_slot >= kCountRing) {
         set_error("uttt_round_hash_async: bad arguments (ring slot must be in 0..%d)", kCountRing - 1);
         return UTTT_ERR_ARG;
@@ -3659,11 +3772,7 @@ int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
     }();
     // round 6: the whole round in one dispatch (k_round1; UTTT_ROUND_DISPATCHES=3 keeps k_round + k_scan +
     // k_hash_leaves)
-    static const bool one = [] {
-        const char *v = getenv("UTTT_ROUND_DISPATCHES");
-        return !(v && v[0] == '3');
-    }();
-    if (fuse && one) {
+    if (one_dispatch_rounds()) {
         if (e->phase != 1) {
             set_error("uttt_round_hash_async: call uttt_search_begin (or apply the previous round) first");
             return UTTT_ERR_ORDER;
@@ -3677,7 +3786,8 @@ int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
         const int apply = e->dev_apply_staged ? 1 : 0;
         timed_launch(e, kKSelect, e->tr.py ? k_round1<true> : k_round1<false>, dim3(grid_waves(e->tr.n_trees)),
                      dim3(kBlock), e->pool, e->tr, e->cache, e->dev_apply_policy, e->dev_apply_value, policy, value, apply,
-                     e->timing ? e->d_bytes : nullptr, e->h_ring + 4 * ring_slot, tag, e->d_r1ctl);
+                     e->timing ? e->d_bytes : nullptr, e->h_ring + 4 * ring_slot, tag, e->d_r1ctl, part_host, part_dev,
+                     part_prev, nb_prev);
         if (int rc0 = check_launch()) return rc0;
         e->dev_apply_policy = policy;
         e->dev_apply_value = value;
