@@ -2600,8 +2600,9 @@ __device__ __forceinline__ void mt_seed_wave(uint32_t *key, int32_t *pos, uint32
 // per slot). A finished game's plies are copied with eight independent loads in flight per thread before
 // their stores (round 4: one dependent load-store pair per iteration, ~19 memory round trips per game, a
 // 39 us launch). seed: the last wave also seeds a refilled slot's key (selfplay_begin and the blocking move
-// end); the asynchronous move end seeds on the engine's side stream instead (k_seed), off the critical path
-// (a key is first drawn from at the next move's end).
+// end, and the asynchronous one by default); UTTT_SEED_STREAM=1 runs the whole kernel on the engine's side
+// stream, off the critical path (a key is first drawn from, and a finished game's rows first overwritten, at
+// the next move's end).
 constexpr int kArchiveBlocks = 256;
 __global__ __launch_bounds__(256) void k_archive(SelfPlay sp, const unsigned long long *err, int seed) {
     if (err && *err != ~0ull) return;
@@ -2636,19 +2637,6 @@ __global__ __launch_bounds__(256) void k_archive(SelfPlay sp, const unsigned lon
     }
 }
 
-// The refilled slots' keys (numpy's init_genrand(seed_base + game)), one wave per work-list entry, on the
-// engine's side stream behind k_finalize (the asynchronous move end); the next move end waits for it.
-__global__ __launch_bounds__(kWave) void k_seed(SelfPlay sp, const unsigned long long *err) {
-    if (err && *err != ~0ull) return;
-    const int n_work = sp.work[0];
-    for (int w = blockIdx.x; w < n_work; w += gridDim.x) {
-        const int s = sp.work[1 + w];
-        const Slot sl = sp.slot[s];
-        if (!sl.seed_pending) continue;
-        mt_seed_wave(sp.mt_key + (size_t)s * 624, sp.mt_pos + s, sp.seed_base + (uint32_t)sl.game);
-        if (lane_id() == 0) sp.slot[s].seed_pending = 0;
-    }
-}
 static int archive_grid(int slots) { return slots < kArchiveBlocks ? slots : kArchiveBlocks; }
 
 __global__ void k_hwc(const uttt_state_t *st, int64_t n, float *out) {
@@ -2738,7 +2726,7 @@ struct uttt_engine {
     };
     std::vector<Ev> pending_ev;
     std::vector<hipEvent_t> ev_pool;
-    // the asynchronous move end's side stream: the refilled slots' key seeding (k_seed) runs there behind
+    // the asynchronous move end's side stream (UTTT_SEED_STREAM=1): k_archive runs there behind
     // k_finalize (ev_fin) and the next move end waits for it (ev_seed, join_seed)
     hipStream_t seed_stream = nullptr;
     hipEvent_t ev_fin = nullptr, ev_seed = nullptr;
@@ -4078,9 +4066,9 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
                            e->pool, e->sp, fail);
         hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, e->stream, e->sp, fail, (const TreeCtl *)e->tr.ctl,
                            e->d_err, e->h_move);
-        // UTTT_SEED_STREAM=1: the refilled slots' keys are seeded on a side stream, overlapping the archive copy
-        // and the next move's rounds, and the next move end joins it (round 6, measured: tree-only +1.3% with
-        // the seed chain at 18 us, headline within noise; after the chain's rewrite k_archive seeds in place)
+        // UTTT_SEED_STREAM=1: k_archive (the finished games' copy to the arena, the refilled slots' keys) runs
+        // on a side stream, overlapping the next move's rounds, which need neither; the next move end and every
+        // reader of the arena or the keys join it (round 6, measured in DESIGN §7)
         static const bool side = [] {
             const char *v = getenv("UTTT_SEED_STREAM");
             return v && v[0] == '1';
@@ -4093,11 +4081,12 @@ int uttt_selfplay_move_end_async(uttt_engine_t *e) {
             }
             HIP_TRY(hipEventRecord(e->ev_fin, e->stream));
             HIP_TRY(hipStreamWaitEvent(e->seed_stream, e->ev_fin, 0));
-            hipLaunchKernelGGL(k_seed, dim3(archive_grid(slots)), dim3(kWave), 0, e->seed_stream, e->sp, err);
+            hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->seed_stream, e->sp, err, 1);
             HIP_TRY(hipEventRecord(e->ev_seed, e->seed_stream));
             e->seed_inflight = true;
+        } else {
+            hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, e->sp, err, 1);
         }
-        hipLaunchKernelGGL(k_archive, dim3(archive_grid(slots)), dim3(256), 0, e->stream, e->sp, err, side ? 0 : 1);
     }
     int rc = check_launch();
     if (rc) return rc;  // k_finalize stored the counters and the failure word into h_move
@@ -4129,6 +4118,7 @@ int uttt_selfplay_games(uttt_engine_t *e, int64_t *game_ids, int64_t *offsets, i
                         int64_t *n_games) {
     if (!e || !e->selfplay) return UTTT_ERR_ORDER;
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc_join = join_seed(e)) return rc_join;
     int64_t ctr[4];
     HIP_TRY(hipMemcpyAsync(ctr, e->sp.ctr, sizeof(ctr), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -4150,6 +4140,7 @@ int uttt_selfplay_plies(uttt_engine_t *e, uttt_state_t *states, double *policies
                         float *inputs_hwc, int64_t max_plies, int64_t *n_plies) {
     if (!e || !e->selfplay) return UTTT_ERR_ORDER;
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc_join = join_seed(e)) return rc_join;
     const int64_t n = std::min<int64_t>(e->sp_arena_used, max_plies);
     if (n_plies) *n_plies = e->sp_arena_used;
     if (n <= 0) return UTTT_OK;
