@@ -84,7 +84,10 @@ enum KernelId {
     kKSelLevels, kKSelTrees, kKSelMax, kKSelMaxSum,
     // dependent memory round trips (the latency model's unit): sum over trees, the current launch's
     // slowest tree, that slowest count summed over launches
-    kKSelTrips, kKSelTripMax, kKSelTripMaxSum, kKernelCount
+    kKSelTrips, kKSelTripMax, kKSelTripMaxSum,
+    // the slowest-tree rows of odd rounds in uttt_rounds_hash_move's per-block form (k_round1 with part_host):
+    // each round folds the previous round's rows at its start, so no round needs a last block
+    kKSelMaxB, kKSelTripMaxB, kKernelCount
 };
 
 // Device counters are striped: counter i of a row lives in kStripes 128-byte slots, and a workgroup
@@ -877,7 +880,7 @@ __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int firs
 // Returns the tree's pending word (wave-uniform), as stored to tr.pending[t].
 template <bool PY>
 __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache, unsigned long long *stats, int t,
-                                           float *cv_row, HostLeaf *host_leaf, int32_t tag) {
+                                           float *cv_row, HostLeaf *host_leaf, int32_t tag, int max_alt = 0) {
     const int lane = lane_id();
     TreeCtl ctl = tr.ctl[t];
     int pend = 0;
@@ -1141,9 +1144,9 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
         if (stats && levels) {
             atomicAdd(stripe_of(stats + kKSelLevels * kRow), (unsigned long long)levels);
             atomicAdd(stripe_of(stats + kKSelTrees * kRow), 1ull);
-            atomicMax(stripe_of(stats + kKSelMax * kRow), (unsigned long long)levels);
+            atomicMax(stripe_of(stats + (max_alt ? kKSelMaxB : kKSelMax) * kRow), (unsigned long long)levels);
             atomicAdd(stripe_of(stats + kKSelTrips * kRow), (unsigned long long)trips);
-            atomicMax(stripe_of(stats + kKSelTripMax * kRow), (unsigned long long)trips);
+            atomicMax(stripe_of(stats + (max_alt ? kKSelTripMaxB : kKSelTripMax) * kRow), (unsigned long long)trips);
         }
         if (host_leaf) {  // one tree: what k_scan would derive from pending[0]
             const int p = pend & 0xFF, c0 = (p == 1 || p == 3) ? 1 : 0, c1 = p == 2 ? 1 : 0, c2 = p >= 2 ? 1 : 0;
@@ -1685,7 +1688,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
                                                    float *__restrict__ value, int apply, unsigned long long *stats,
                                                    int32_t *host_count, int32_t tag, uint32_t *rctl,
                                                    uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev,
-                                                   int nb_prev) {
+                                                   int nb_prev, int stats_parity) {
     __shared__ __attribute__((aligned(16))) float s_row[kWavesPerBlock][84];
     __shared__ uint32_t s_cnt;
     __shared__ int s_last;
@@ -1694,6 +1697,30 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
     // empty-round check reads, part_prev), and the host sums the words once every block's has the tag: the
     // arrival atomics, the partials' reload and the last block's drain left each round's critical path (round 6)
     if (part_host) {
+        if (stats && blockIdx.x == 0 && threadIdx.x < kWave) {
+            // the previous round's slowest tree (the other parity's rows) into the sums; this round's waves
+            // write this parity's rows meanwhile
+            const int rm = stats_parity ? kKSelMax : kKSelMaxB, rt = stats_parity ? kKSelTripMax : kKSelTripMaxB;
+            unsigned long long ml = 0ull, mt = 0ull;
+            if (threadIdx.x < kStripes) {
+                unsigned long long *a = stats + rm * kRow + threadIdx.x * kStripeStride;
+                unsigned long long *bb = stats + rt * kRow + threadIdx.x * kStripeStride;
+                ml = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                mt = __hip_atomic_load(bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(bb, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const unsigned long long ol = __shfl_xor(ml, off), ot = __shfl_xor(mt, off);
+                ml = ol > ml ? ol : ml;
+                mt = ot > mt ? ot : mt;
+            }
+            if (threadIdx.x == 0) {
+                stats[kKSelMaxSum * kRow] += ml;
+                stats[kKSelTripMaxSum * kRow] += mt;
+            }
+        }
         const uint32_t t17 = ((uint32_t)tag & kPartTagMask) << kPartTagShift;
         bool empty = false;
         if (part_prev) {  // the previous round queued no leaf and left no tree with simulations
@@ -1736,7 +1763,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
                        false, &held);
             wave_memory_fence();  // the descent reads the records the apply wrote
         }
-        const int p = select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0);
+        const int p = select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0,
+                                      part_host ? stats_parity : 0);
         if (p & 1) {
             wave_memory_fence();  // lane 0 stored the leaf
             const uttt_state_t leaf = tr.leaf[t];
@@ -2689,6 +2717,7 @@ struct uttt_engine {
     // [2][part_cap] (the previous round's, for the empty-round check)
     uint32_t *h_part = nullptr, *d_part = nullptr;
     int32_t part_cap = 0;
+    uint32_t round_parity = 0;  // the per-block rounds' select-statistics parity (alternates every round)
     int32_t host_apply_rows = 0;  // a one-tree evaluation staged by uttt_search_apply_host, applied by the next
                                   // k_flush1 (or by flush_host_apply before any other call that reads the tree)
     int32_t leaf_tag = 0;
@@ -3616,7 +3645,8 @@ int uttt_rounds_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, flo
 }
 
 static int round_hash_async_impl(uttt_engine *e, int32_t ring_slot, int32_t tag, float *policy, float *value,
-                                 uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev, int nb_prev);
+                                 uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev, int nb_prev,
+                                 int stats_parity = 0);
 
 static bool one_dispatch_rounds() {  // k_round1 (UTTT_ROUND_DISPATCHES=3 / UTTT_FUSED_ROUNDS=0: the round-5 forms)
     static const bool one = [] {
@@ -3635,12 +3665,13 @@ int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
         return UTTT_ERR_ARG;
     }
     // per-block count words (k_round1's part_host form: no last-block publish; UTTT_ROUND_PARTS=0 keeps the ring
-    // slot's counts); not with kernel timing, whose select statistics the last block folds
+    // slot's counts); with kernel timing, each round folds the previous round's select statistics (rows by
+    // round parity) at its start
     static const bool parts_env = [] {
         const char *v = getenv("UTTT_ROUND_PARTS");
         return !(v && v[0] == '0');
     }();
-    const bool parts = parts_env && one_dispatch_rounds() && !e->timing;
+    const bool parts = parts_env && one_dispatch_rounds();
     const int nb = grid_waves(e->tr.n_trees);
     if (parts && !e->h_part) {
         const int cap = grid_waves(e->max_trees);
@@ -3661,7 +3692,8 @@ int uttt_rounds_hash_move(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
         const int slot = (ring_slot + enq) % kCountRing;
         const int rc = parts ? round_hash_async_impl(e, slot, tag_of(enq), policy, value, e->h_part + (size_t)slot * cap,
                                                      e->d_part + (size_t)(enq & 1) * cap,
-                                                     enq ? e->d_part + (size_t)((enq - 1) & 1) * cap : nullptr, nb)
+                                                     enq ? e->d_part + (size_t)((enq - 1) & 1) * cap : nullptr, nb,
+                                                     (e->round_parity++) & 1)
                              : uttt_round_hash_async(e, slot, tag_of(enq), policy, value);
         if (rc == UTTT_OK) ++enq;
         return rc;
@@ -3746,10 +3778,11 @@ int uttt_round_hash_async(uttt_engine_t *e, int32_t ring_slot, int32_t tag, floa
     return round_hash_async_impl(e, ring_slot, tag, policy, value, nullptr, nullptr, nullptr, 0);
 }
 
-// part_host != nullptr (uttt_rounds_hash_move only, with the one-dispatch rounds and no kernel timing): the
-// round's counts go to per-block words instead of the ring slot (k_round1's part_host form)
+// part_host != nullptr (uttt_rounds_hash_move only, with the one-dispatch rounds): the round's counts go to
+// per-block words instead of the ring slot (k_round1's part_host form)
 static int round_hash_async_impl(uttt_engine *e, int32_t ring_slot, int32_t tag, float *policy, float *value,
-                                 uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev, int nb_prev) {
+                                 uint32_t *part_host, uint32_t *part_dev, const uint32_t *part_prev, int nb_prev,
+                                 int stats_parity) {
     if (!e || !policy || !value || ring_slot < 0 || ring_slot >= kCountRing) {
         set_error("uttt_round_hash_async: bad arguments (ring slot must be in 0..%d)", kCountRing - 1);
         return UTTT_ERR_ARG;
@@ -3775,7 +3808,7 @@ static int round_hash_async_impl(uttt_engine *e, int32_t ring_slot, int32_t tag,
         timed_launch(e, kKSelect, e->tr.py ? k_round1<true> : k_round1<false>, dim3(grid_waves(e->tr.n_trees)),
                      dim3(kBlock), e->pool, e->tr, e->cache, e->dev_apply_policy, e->dev_apply_value, policy, value, apply,
                      e->timing ? e->d_bytes : nullptr, e->h_ring + 4 * ring_slot, tag, e->d_r1ctl, part_host, part_dev,
-                     part_prev, nb_prev);
+                     part_prev, nb_prev, stats_parity);
         if (int rc0 = check_launch()) return rc0;
         e->dev_apply_policy = policy;
         e->dev_apply_value = value;
