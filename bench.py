@@ -656,7 +656,9 @@ def main():
                         # SURVEY §8(d) kernel microbench: the search kernels alone (hash evaluator, no network),
                         # one lane: with no network to overlap, one launch per round over every tree is the
                         # fastest shape (1 / 2 / 4 lanes: 170.6M / 141M / 82M sims/s, profiles/r3/ab/hashlanes.log)
-                        ("tree_only_4096x50", dict(evaluator="hash", age=100, lanes=1)),
+                        # 60 timed moves (as the standalone tree-only runs): 10 are a 3 ms window, where the
+                        # window's own start and end set a tenth of the rate
+                        ("tree_only_4096x50", dict(evaluator="hash", age=100, lanes=1, steps=60)),
                         # SURVEY §8(f) rank 1's optional fast evaluator: the tower conv with one f16 product per
                         # point (uttt_nn_conv3x3_wino3h_f16, ~1e-3 relative): not the reference's numerics, so a
                         # variant line beside the f32-level headline, never the headline
