@@ -2279,27 +2279,17 @@ __device__ double np_sum(const double *a, int n, int stride) {
     return res;  // n <= 81 < 128: a single pairwise block
 }
 
-// A double held by lane i of the wave (i uniform), to every lane: the sequential f64 sums below run
-// the reference's additions in its order on values spread over the lanes, without an LDS round trip.
-__device__ __forceinline__ double lane_double(double x, int i) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), i);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
+// A float held by lane i of the wave (i uniform), to every lane.
 __device__ __forceinline__ float lane_float(float x, int i) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), i));
-}
-// entry i of a row held as two halves (lane i: x0, lane i - 64: x1)
-__device__ __forceinline__ double row_entry(double x0, double x1, int i) {
-    return i < 64 ? lane_double(x0, i) : lane_double(x1, i - 64);
 }
 
 // One wave per slot: the per-move tail of self_play_cpp.play (:63-92). Entry i of the root's score
 // row lives in lane i (x0) and lane i - 64 (x1); what is order-free (the arg-max, the f32 sum of
 // integer visit counts) is a wave reduction, what is not (np.sum's pairwise blocks, the cumsum of
-// np.random.choice) runs the reference's additions in its order on readlane operands, the same in
-// every lane. Round 3's thread-per-slot form walked the row in LDS, 81-step dependent chains per pass.
+// np.random.choice) runs the reference's additions in its order on the wave's LDS copy of the row, the
+// same in every lane (round 5: on v_readlane operands; round 3's thread-per-slot form walked the row in
+// LDS, 81-step dependent chains per pass with one wave per 64 slots).
 // fail (the asynchronous form: the search's failure flag, Trees::count[3]): on a failure this move's end
 // changes nothing (no draw, no record, no refill), as the blocking form refuses before it runs
 __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, const int32_t *fail) {
@@ -2381,35 +2371,48 @@ __global__ __launch_bounds__(kBlock) void k_move_end(Pool pool, SelfPlay sp, con
         x0 = (double)v0;
         x1 = (double)v1;
     }
+    // The row's entries for the sequential f64 sums below go through this wave's LDS row (entry i at xr[i],
+    // read at a uniform address): a load and an add per entry, where the v_readlane pair, the select of the
+    // half and the prefix's lane select per entry made the move end VALU-issue bound (round 6; every lane
+    // still runs the same additions in the same order)
+    __shared__ double s_xrow[kWavesPerBlock][81];
+    double *const xr = s_xrow[threadIdx.x >> 6];
+    auto stage = [&]() {
+        if (h0) xr[lane] = x0;
+        if (h1) xr[64 + lane] = x1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's stores before any lane's reads
+    };
+    stage();
     // scores -> float64, renormalised with np.sum (:74-78): np.add.reduce's pairwise block (8
     // accumulators over i = j mod 8, then the remainder), the same additions in every lane
     double tot;
     if (L < 8) {
         tot = 0.0;
-        for (int i = 0; i < L; ++i) tot += row_entry(x0, x1, i);
+        for (int i = 0; i < L; ++i) tot += xr[i];
     } else {
         double r[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] = lane_double(x0, j);
+        for (int j = 0; j < 8; ++j) r[j] = xr[j];
         int i = 8;
         for (; i < L - (L % 8); i += 8)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) r[j] += row_entry(x0, x1, i + j);
+            for (int j = 0; j < 8; ++j) r[j] += xr[i + j];
         tot = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < L; ++i) tot += row_entry(x0, x1, i);
+        for (; i < L; ++i) tot += xr[i];
     }
     x0 = h0 ? ((tot == 0.0) ? 1.0 / (double)L : x0 / tot) : 0.0;
     x1 = h1 ? ((tot == 0.0) ? 1.0 / (double)L : x1 / tot) : 0.0;
+    stage();
     // np.random.choice(legal, p=d) (:86): cdf = cumsum; cdf /= cdf[-1]; searchsorted right. The
-    // cumsum's prefixes land in the lanes of their entries; its last prefix is cdf[-1].
-    double c0 = 0.0, c1 = 0.0, acc = 0.0;
+    // cumsum's prefixes are written over the row in place and land in the lanes of their entries; its last
+    // prefix is cdf[-1].
+    double acc = 0.0;
     for (int i = 0; i < L; ++i) {
-        acc += row_entry(x0, x1, i);
-        if (lane == (i & 63)) {
-            if (i < 64) c0 = acc;
-            else c1 = acc;
-        }
+        acc += xr[i];
+        xr[i] = acc;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const double c0 = h0 ? xr[lane] : 0.0, c1 = h1 ? xr[64 + lane] : 0.0;
     const uint64_t b0 = __ballot(h0 && !(c0 / acc <= u)), b1 = __ballot(h1 && !(c1 / acc <= u));
     const int k = b0 ? __builtin_ctzll(b0) : (b1 ? 64 + __builtin_ctzll(b1) : L - 1);  // idx >= L -> L - 1
     // policy target (:81-83): entry i of the row goes to the i-th legal action, the rest are zero
