@@ -2469,6 +2469,22 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const int32_t *f
     __shared__ unsigned long long wsum[32];
     __shared__ int s_work;  // entries of k_archive's work list
     __shared__ unsigned long long s_first;
+    const int tid = threadIdx.x;
+    // the counters are read before the scans (only this kernel writes them, after its last barrier): their
+    // round trip overlaps the slots' instead of following the scans
+    const int64_t arena0 = sp.ctr[2], games0 = sp.ctr[1], next0 = sp.ctr[0];
+    const int per = (sp.slots + 1023) / 1024;
+    const int b = tid * per, e = min(b + per, sp.slots);
+    // the scans need a slot's live / finished / fin_len only: one 16-byte load of Slot bytes 40..55 per slot
+    // (up to kFinPer per thread, all in flight together, kept for the second pass), and the second pass
+    // reads and rewrites only the slots that change (a game just finished or the slot is free); every other
+    // slot was brought up to date by k_move_end. Round 5: the single block read and wrote every 80-byte
+    // slot through one CU (31 us per move at 4,096 slots). They go out with the failure word's load (round 6).
+    constexpr int kFinPer = 4;
+    int4 hot[kFinPer];
+#pragma unroll
+    for (int j = 0; j < kFinPer; ++j)
+        if (b + j < e) hot[j] = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(sp.slot + b + j) + 40);
     if (fail && *fail) {
         if (threadIdx.x == 0) s_first = ~0ull;
         __syncthreads();
@@ -2483,22 +2499,6 @@ __global__ __launch_bounds__(1024) void k_finalize(SelfPlay sp, const int32_t *f
         }
         return;
     }
-    const int tid = threadIdx.x;
-    // the counters are read before the scans (only this kernel writes them, after its last barrier): their
-    // round trip overlaps the slots' instead of following the scans
-    const int64_t arena0 = sp.ctr[2], games0 = sp.ctr[1], next0 = sp.ctr[0];
-    const int per = (sp.slots + 1023) / 1024;
-    const int b = tid * per, e = min(b + per, sp.slots);
-    // the scans need a slot's live / finished / fin_len only: one 16-byte load of Slot bytes 40..55 per slot
-    // (up to kFinPer per thread, all in flight together, kept for the second pass), and the second pass
-    // reads and rewrites only the slots that change (a game just finished or the slot is free); every other
-    // slot was brought up to date by k_move_end. Round 5: the single block read and wrote every 80-byte
-    // slot through one CU (31 us per move at 4,096 slots).
-    constexpr int kFinPer = 4;
-    int4 hot[kFinPer];
-#pragma unroll
-    for (int j = 0; j < kFinPer; ++j)
-        if (b + j < e) hot[j] = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(sp.slot + b + j) + 40);
     auto hot_of = [&](int i) -> int4 {
         return i - b < kFinPer ? hot[i - b] : *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(sp.slot + i) + 40);
     };
@@ -2636,10 +2636,15 @@ __device__ __forceinline__ void mt_seed_wave(uint32_t *key, int32_t *pos, uint32
 // the next move's end).
 constexpr int kArchiveBlocks = 256;
 __global__ __launch_bounds__(256) void k_archive(SelfPlay sp, const unsigned long long *err, int seed) {
-    if (err && *err != ~0ull) return;
+    // the failure word, the list's length and this block's first entry are loaded together (the grid is at
+    // most the slot count and the list has room for every slot, so entry blockIdx.x is in bounds): one round
+    // trip before the first slot load instead of three
+    const unsigned long long e0 = err ? *err : ~0ull;
     const int n_work = sp.work[0];
+    const int first = sp.work[1 + blockIdx.x];
+    if (e0 != ~0ull) return;
     for (int w = blockIdx.x; w < n_work; w += gridDim.x) {
-        const int s = sp.work[1 + w];
+        const int s = w == (int)blockIdx.x ? first : sp.work[1 + w];
         const Slot sl = sp.slot[s];
         const int wave = (int)threadIdx.x >> 6;
         if (seed && sl.seed_pending && wave == 3) {
