@@ -883,14 +883,20 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                                            float *cv_row, HostLeaf *host_leaf, int32_t tag, int max_alt = 0) {
     const int lane = lane_id();
     TreeCtl ctl = tr.ctl[t];
+    // the root's state and record go out with the control word (round 6: they were a second dependent round
+    // trip after the status check; a tree with nothing to do discards them)
+    const size_t base = (size_t)t * pool.cap;
+    uint4 *__restrict__ R = pool.rec + base;
+    const uttt_state_t root = tr.root[t];
+    const uint4 root_first = R[0];
     int pend = 0;
     unsigned long long bytes = 0;
     unsigned int levels = 0;
     // cache hits / misses of this tree, counted once at the end: an atomic per hit made the next
     // descent's first load wait for it (vmcnt counts the atomic), ~2k cycles a descent (round 4)
     unsigned int hits = 0, misses = 0;
-    // dependent round trips of this wave: the control loads, then per descent the root's link and visits,
-    // one per child-scan group, and for a completion in place the cache probe, payload and re-check,
+    // dependent round trips of this wave: the control loads (with the root's state and record), then per
+    // descent one per child-scan group, and for a completion in place the cache probe, payload and re-check,
     // the path's read-modify-write and the fence
     unsigned int trips = 1;
     SelClock clk;
@@ -904,26 +910,21 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
 #endif
     clk.start();
     if ((ctl.status & kLive) && !(ctl.status & kErrMask) && ctl.sims_done < tr.sims) {
-        const size_t base = (size_t)t * pool.cap;
-        uint4 *__restrict__ R = pool.rec + base;
-        const uttt_state_t root = tr.root[t];
         clk.mark<kSpRootState>();
         int sims_done = ctl.sims_done;
         int budget = tr.budget;
-        // the root's record after this wave's own last back-up (no other wave writes this tree's
-        // nodes during the launch): later descents start from it instead of reloading R[0]
-        uint4 root_rec = make_uint4(0u, 0u, 0u, 0u);
-        bool root_known = false;
+        // the root's record: as loaded with the control word, then after this wave's own last back-up (no
+        // other wave writes this tree's nodes during the launch): no descent reloads R[0]
+        uint4 root_rec = root_first;
         for (;;) {
             uttt_state_t s = root;
             int node = 0, depth = 0;
             int path_lo = 0, path_hi = 0;  // lane d: path[d], path[64 + d]
             // the current node's meta (visits, action, L) and link (below the root: from the parent's scan)
-            const uint4 r0 = root_known ? root_rec : R[0];
+            const uint4 r0 = root_rec;
             uint2 nm = make_uint2(r0.z, r0.w);
             // lane d: the record of path[d] (prec_lo) and path[64 + d] (prec_hi) as read on the way down
             uint4 prec_lo = r0, prec_hi = make_uint4(0u, 0u, 0u, 0u);
-            trips += root_known ? 0u : 1u;
             clk.mark<kSpRoot>();
             bool fail = false;
             int pa = -1;  // a winning action whose next_state is pending (applied under the next loads)
@@ -1057,7 +1058,6 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                                       (uint32_t)__builtin_amdgcn_readlane((int)nl.y, 0),
                                       (uint32_t)__builtin_amdgcn_readlane((int)nl.z, 0),
                                       (uint32_t)__builtin_amdgcn_readlane((int)nl.w, 0));
-                root_known = true;
                 wave_memory_fence();
                 trips += 2;
                 bytes += 16ull * (unsigned long long)(depth + 1);
@@ -1090,7 +1090,6 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                     }
                     break;
                 }
-                root_known = true;
                 clk.mark<kSpExpand>();
                 wave_memory_fence();
                 ++hits;
