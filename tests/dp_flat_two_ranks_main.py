@@ -37,7 +37,7 @@ if __name__ == "__main__":
     # near-zero-variance channels, tests/rccl_one_rank_main.py), Adam with eps = 1e3 and lr 10 (updates ~1e-2
     # m_hat, linear in the gradient): weights within 1% of their motion, each update within 2%.
     from uttt_amd.model import calibrated_network
-    from uttt_amd.train import DPGraphedStep, local_slice, policy_loss_fn
+    from uttt_amd.train import DPGraphedStep, all_reduce_sum, local_slice, policy_loss_fn
     dev = torch.device("cuda", local)
     netcal = os.path.join(REPO, "tests", "golden", "netcal.npz")
     g = torch.Generator(device="cpu").manual_seed(3)
@@ -75,7 +75,7 @@ if __name__ == "__main__":
             step.loss_sum.zero_()
             step.step(mine, len(mine) / 32)
             lt = step.loss_sum.clone()
-            torch.distributed.all_reduce(lt)
+            all_reduce_sum(lt)
             opt_r.zero_grad()
             le = emulate(ref, idx)
             lg = float(lt)

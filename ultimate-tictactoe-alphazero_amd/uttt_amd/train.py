@@ -186,6 +186,19 @@ class GraphedStep:
                 self._body(idx)
 
 
+def all_reduce_sum(t):
+    """dist.all_reduce(t) (SUM) in place. gloo with a device tensor (ranks sharing a GPU: the multi-rank GPU
+    tests' form) goes through an explicit, synchronous host copy, so the collective never depends on gloo's
+    own device streams and pinned staging buffers (round 6: one run in ~30 of tests/dp_flat_two_ranks_main.py
+    read a NaN loss there, cause not found). RCCL and host tensors take dist.all_reduce directly."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t)
+
+
 class DPGraphedStep:
     """The data-parallel step of a torchrun rank as two HIP graphs around ONE collective (round 5):
 
@@ -273,14 +286,14 @@ class DPGraphedStep:
             self.idx.copy_(idx, non_blocking=True)
             self.g_fb.replay()
             if self.collective:
-                dist.all_reduce(self.flat)
+                all_reduce_sum(self.flat)
             self.g_opt.replay()
             return
         sh = torch.full((), float(share), device=self.flat.device)
         with torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=False):
             self._fb(idx, sh)
         if self.collective:
-            dist.all_reduce(self.flat)
+            all_reduce_sum(self.flat)
         self.opt.step()
 
     def sync_buffers(self):
@@ -297,7 +310,7 @@ class DPGraphedStep:
             for m in bns:
                 parts += [m.running_mean.reshape(-1), (m.running_var + m.running_mean * m.running_mean).reshape(-1)]
             flat = torch.cat(parts)
-            dist.all_reduce(flat)
+            all_reduce_sum(flat)
             flat /= self.world
             o = 0
             for m in bns:
@@ -419,7 +432,7 @@ def _train_dp_flat(model, x, p, v, epochs, batch_size, device, seed, lr, log, gr
             o += len(li)
         total = step.loss_sum.clone()
         if world > 1:
-            dist.all_reduce(total)
+            all_reduce_sum(total)
         step.sync_buffers()
         losses.append(float(total) / len(idxs))
         if log and rank == 0:
