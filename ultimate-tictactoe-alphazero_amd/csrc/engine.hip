@@ -880,7 +880,10 @@ __device__ __forceinline__ void puct_group(const uint4 *__restrict__ R, int firs
 // Returns the tree's pending word (wave-uniform), as stored to tr.pending[t].
 template <bool PY>
 __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache, unsigned long long *stats, int t,
-                                           float *cv_row, HostLeaf *host_leaf, int32_t tag, int max_alt = 0) {
+                                           float *cv_row, HostLeaf *host_leaf, int32_t tag, int max_alt = 0,
+                                           uttt_state_t *leaf_out = nullptr) {
+    // leaf_out (k_round1): a queued leaf's state as stored to tr.leaf[t], so the caller's evaluation reads it
+    // from registers (round 6: a store drain and a reload of tr.leaf[t] ended every tree's round)
     const int lane = lane_id();
     TreeCtl ctl = tr.ctl[t];
     // the root's state and record go out with the control word (round 6: they were a second dependent round
@@ -1124,6 +1127,7 @@ __device__ __forceinline__ int select_wave(Pool pool, Trees tr, EvalCache cache,
                 tr.rec[t] = r;
                 tr.leaf[t] = s;
             }
+            if (leaf_out) *leaf_out = s;
             // the probe's flags, the queued path (indices and records), LeafRec and state
             bytes += (cache.flag ? 32ull : 0ull) + 20ull * (unsigned long long)(depth + 1) + 48ull;
             // 3: this leaf's k simulations leave the tree more to do (after its apply)
@@ -1762,13 +1766,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_round1(Pool pool, Trees tr, EvalC
                        false, &held);
             wave_memory_fence();  // the descent reads the records the apply wrote
         }
+        uttt_state_t leaf;
         const int p = select_wave<PY>(pool, tr, cache, stats, t, s_row[threadIdx.x >> 6], nullptr, 0,
-                                      part_host ? stats_parity : 0);
-        if (p & 1) {
-            wave_memory_fence();  // lane 0 stored the leaf
-            const uttt_state_t leaf = tr.leaf[t];
-            hash_leaf_row(leaf, policy, value, t);
-        }
+                                      part_host ? stats_parity : 0, &leaf);
+        if (p & 1) hash_leaf_row(leaf, policy, value, t);  // the queued leaf (its state from the descent)
         const int q = p & 0xFF;
         if (lane == 0)  // pending | stopped << 10 | left << 20 (at most kWavesPerBlock each)
             atomicAdd(&s_cnt, (uint32_t)((q == 1 || q == 3) ? 1 : 0) | ((q == 2 ? 1u : 0u) << 10) |
